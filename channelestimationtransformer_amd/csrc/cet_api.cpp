@@ -1,0 +1,1010 @@
+// Host runtime behind include/cet.h: weight intake by reference key name, packing into
+// MFMA fragment order, execution plans, the torch-compatible ProbSparse sampler and the
+// per-forward key-multiplicity tables.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/cet.h"
+#include "cet_kernels.h"
+#include "cet_plan.hpp"
+
+using namespace cet;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(CET_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// ------------------------------------------------------------------ torch CPU generator
+// torch.manual_seed(s) seeds an mt19937 with (uint32)s; CPU randint(L, shape) draws
+// mt19937() % L sequentially (verified against torch in tests/test_rng_native.py).
+struct MT19937 {
+  uint32_t mt[624];
+  int idx = 624;
+  void seed(uint64_t s) {
+    mt[0] = (uint32_t)(s & 0xffffffffu);
+    for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    idx = 624;
+  }
+  uint32_t next() {
+    if (idx >= 624) {
+      for (int i = 0; i < 624; ++i) {
+        const uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+        mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      idx = 0;
+    }
+    uint32_t y = mt[idx++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+};
+
+uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+int r16(int x) { return (x + 15) & ~15; }
+int r32(int x) { return (x + 31) & ~31; }
+int u_part(int factor, int L) {
+  const int u = factor * (int)std::ceil(std::log((double)L));
+  return u < L ? u : L;
+}
+
+struct Weight {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+  bool loaded = false;
+  bool required = true;
+};
+
+}  // namespace
+
+struct cet_engine {
+  int kind = 0;  // 0 informer, 1 transformer
+  cet_informer_config icfg{};
+  cet_transformer_config tcfg{};
+  std::map<std::string, Weight> weights;
+  std::vector<std::string> order;
+  bool dirty = true;
+  bool uploaded = false;
+
+  // packed blobs
+  std::vector<uint16_t> wblob;
+  std::vector<float> pblob;
+  InformerPlan ip{};
+  TransformerPlan tp{};
+  void* d_plan = nullptr;
+  void* d_w = nullptr;
+  float* d_p = nullptr;
+  size_t d_w_bytes = 0, d_p_bytes = 0;
+
+  // ProbSparse sampling
+  struct Call { int LK, LQ, U; };
+  std::vector<Call> calls;
+  std::vector<std::vector<int32_t>> idx;
+  std::vector<bool> idx_set;
+  bool native_rng = false;
+  MT19937 rng;
+
+  // per-forward multiplicity tables (ring of pinned staging + device buffers)
+  static constexpr int NSLOT = 4;
+  uint8_t* h_cnt[NSLOT] = {};
+  uint8_t* d_cnt[NSLOT] = {};
+  hipEvent_t ev[NSLOT] = {};
+  bool ev_used[NSLOT] = {};
+  int slot = 0;
+  size_t cnt_bytes = 0;
+
+  float* dbg = nullptr;
+  std::string dbg_json;
+  int64_t attn_floats = 0;
+  std::vector<std::pair<int64_t, int>> attn_layout;  // (offset, L) per encoder layer
+
+  ~cet_engine() {
+    if (d_plan) (void)hipFree(d_plan);
+    if (d_w) (void)hipFree(d_w);
+    if (d_p) (void)hipFree(d_p);
+    for (int i = 0; i < NSLOT; ++i) {
+      if (h_cnt[i]) (void)hipHostFree(h_cnt[i]);
+      if (d_cnt[i]) (void)hipFree(d_cnt[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+  }
+
+  void add(const std::string& name, std::vector<int64_t> shape, bool required = true) {
+    Weight w;
+    w.shape = std::move(shape);
+    w.required = required;
+    weights[name] = std::move(w);
+    order.push_back(name);
+  }
+  const std::vector<float>& W(const std::string& n) const { return weights.at(n).data; }
+  float scalar(const std::string& n) const { return weights.at(n).data.at(0); }
+  bool has(const std::string& n) const {
+    auto it = weights.find(n);
+    return it != weights.end() && it->second.loaded;
+  }
+};
+
+namespace {
+
+// ------------------------------------------------------------------ schema (mirrors spec.py)
+void schema_embedding(cet_engine* e, const std::string& p, int c_in, int d) {
+  e->add(p + ".value_embedding.tokenConv.weight", {d, c_in, 3});
+  e->add(p + ".value_embedding.tokenConv.bias", {d});
+  e->add(p + ".position_embedding.pe", {1, 5000, d});
+  // temporal tables (embed.py:130-159) exist in checkpoints but are never used (embed.py:132-135)
+  const char* names[4] = {"hour_embed", "weekday_embed", "day_embed", "month_embed"};
+  const int rows[4] = {24, 7, 32, 13};
+  for (int i = 0; i < 4; ++i) e->add(p + ".temporal_embedding." + names[i] + ".emb.weight", {rows[i], d}, false);
+}
+
+void schema_attn(cet_engine* e, const std::string& p, int d, bool lsq) {
+  for (const char* n : {"query_projection", "key_projection", "value_projection", "out_projection"}) {
+    e->add(p + "." + n + ".weight", {d, d});
+    e->add(p + "." + n + ".bias", {d});
+    if (lsq) e->add(p + "." + n + ".step_size", {});
+  }
+}
+
+void schema_ffn(cet_engine* e, const std::string& p, int d, int dff, bool lsq) {
+  e->add(p + ".conv1.weight", {dff, d, 1});
+  e->add(p + ".conv1.bias", {dff});
+  if (lsq) e->add(p + ".conv1.step_size", {});
+  e->add(p + ".conv2.weight", {d, dff, 1});
+  e->add(p + ".conv2.bias", {d});
+  if (lsq) e->add(p + ".conv2.step_size", {});
+}
+
+void schema_ln(cet_engine* e, const std::string& p, int d) {
+  e->add(p + ".weight", {d});
+  e->add(p + ".bias", {d});
+}
+
+void schema_informer(cet_engine* e) {
+  const auto& c = e->icfg;
+  const int d = c.d_model;
+  const bool lsq = c.lsq_bits > 0;
+  schema_embedding(e, "enc_embedding", c.enc_in, d);
+  schema_embedding(e, "dec_embedding", c.dec_in, d);
+  for (int i = 0; i < c.n_enc; ++i) {
+    const std::string pre = c.stack ? "encoder.encoders." + std::to_string(i) : std::string("encoder");
+    for (int l = 0; l < c.e_layers[i]; ++l) {
+      const std::string p = pre + ".attn_layers." + std::to_string(l);
+      schema_attn(e, p + ".attention", d, lsq);
+      schema_ffn(e, p, d, c.d_ff, lsq);
+      schema_ln(e, p + ".norm1", d);
+      schema_ln(e, p + ".norm2", d);
+    }
+    if (c.distil)
+      for (int l = 0; l < c.e_layers[i] - 1; ++l) {
+        const std::string p = pre + ".conv_layers." + std::to_string(l);
+        e->add(p + ".downConv.weight", {d, d, 3});
+        e->add(p + ".downConv.bias", {d});
+        if (lsq) e->add(p + ".downConv.step_size", {});
+        e->add(p + ".norm.weight", {d});
+        e->add(p + ".norm.bias", {d});
+        e->add(p + ".norm.running_mean", {d});
+        e->add(p + ".norm.running_var", {d});
+        e->add(p + ".norm.num_batches_tracked", {}, false);
+      }
+    schema_ln(e, pre + ".norm", d);
+  }
+  for (int l = 0; l < c.d_layers; ++l) {
+    const std::string p = "decoder.layers." + std::to_string(l);
+    schema_attn(e, p + ".self_attention", d, lsq);
+    schema_attn(e, p + ".cross_attention", d, lsq);
+    schema_ffn(e, p, d, c.d_ff, lsq);
+    schema_ln(e, p + ".norm1", d);
+    schema_ln(e, p + ".norm2", d);
+    schema_ln(e, p + ".norm3", d);
+  }
+  schema_ln(e, "decoder.norm", d);
+  e->add("projection.weight", {c.c_out, d});
+  e->add("projection.bias", {c.c_out});
+}
+
+void schema_transformer(cet_engine* e) {
+  const auto& c = e->tcfg;
+  const int d = c.d_model;
+  auto mha = [&](const std::string& p) {
+    for (const char* n : {"w_q", "w_k", "w_v", "w_o"}) e->add(p + "." + n + ".weight", {d, d});
+  };
+  auto ff = [&](const std::string& p) {
+    e->add(p + ".linear_1.weight", {c.d_ff, d});
+    e->add(p + ".linear_1.bias", {c.d_ff});
+    e->add(p + ".linear_2.weight", {d, c.d_ff});
+    e->add(p + ".linear_2.bias", {d});
+  };
+  auto ln = [&](const std::string& p) {
+    e->add(p + ".alpha", {d});
+    e->add(p + ".bias", {d});
+  };
+  for (int l = 0; l < c.N; ++l) {
+    const std::string p = "encoder.layers." + std::to_string(l);
+    mha(p + ".self_attention_block");
+    ff(p + ".feed_forward_block");
+    for (int r = 0; r < 2; ++r) ln(p + ".residual_connections." + std::to_string(r) + ".norm");
+  }
+  ln("encoder.norm");
+  for (int l = 0; l < c.N; ++l) {
+    const std::string p = "decoder.layers." + std::to_string(l);
+    mha(p + ".self_attention_block");
+    mha(p + ".cross_attention_block");
+    ff(p + ".feed_forward_block");
+    for (int r = 0; r < 3; ++r) ln(p + ".residual_connections." + std::to_string(r) + ".norm");
+  }
+  ln("decoder.norm");
+  e->add("src_embed.tokenEmbedding.weight", {d, c.src_vocab, 3});
+  e->add("src_embed.tokenEmbedding.bias", {d});
+  e->add("tgt_embed.tokenEmbedding.weight", {d, c.tgt_vocab, 3});
+  e->add("tgt_embed.tokenEmbedding.bias", {d});
+  e->add("src_pos.pe", {1, c.src_seq_len, d});
+  e->add("tgt_pos.pe", {1, c.tgt_seq_len + c.label_len, d});
+  e->add("projection_layer.proj.weight", {c.tgt_vocab, d});
+  e->add("projection_layer.proj.bias", {c.tgt_vocab});
+}
+
+// ------------------------------------------------------------------ packing
+struct Packer {
+  std::vector<uint16_t>& wb;
+  std::vector<float>& pb;
+
+  // W given as a row-major [N][K] fp32 matrix → fragment order [N/16][K/32][64][8] bf16.
+  GemmDesc gemm(const std::vector<float>& w, int N, int K, const float* bias, const float* scale) {
+    GemmDesc d{};
+    const int Np = r16(N), Kp = r32(K);
+    d.w = (uint32_t)(wb.size() / 8);
+    d.n = (uint16_t)Np;
+    d.k = (uint16_t)Kp;
+    for (int nt = 0; nt < Np / 16; ++nt)
+      for (int ks = 0; ks < Kp / 32; ++ks)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int n = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
+            wb.push_back(n < N && k < K ? f2bf(w[(size_t)n * K + k]) : 0);
+          }
+    d.bias = bias ? vec(bias, N, Np) : NONE;
+    d.scale = scale ? vec(scale, N, Np) : NONE;
+    return d;
+  }
+  uint32_t vec(const float* v, int n, int npad) {
+    while (pb.size() % 4) pb.push_back(0.f);
+    const uint32_t off = (uint32_t)pb.size();
+    for (int i = 0; i < npad; ++i) pb.push_back(i < n ? v[i] : 0.f);
+    return off;
+  }
+  LNDesc ln(const std::vector<float>& g, const std::vector<float>& b) {
+    LNDesc d;
+    d.g = vec(g.data(), (int)g.size(), (int)g.size());
+    d.b = vec(b.data(), (int)b.size(), (int)b.size());
+    return d;
+  }
+};
+
+// LSQ weight grid (LSQ.py:65-74): q = round_half_even(clamp(w/s, Qn, Qp)); w_q = q·s.  The
+// integer q (exact in bf16 for |q| ≤ 256) is packed and s is applied in the epilogue.
+void lsq_grid(std::vector<float>& w, float s, int bits) {
+  const float qn = -(float)(1 << (bits - 1)), qp = (float)((1 << (bits - 1)) - 1);
+  for (auto& x : w) {
+    float v = x / s;
+    v = v < qn ? qn : (v > qp ? qp : v);
+    x = std::nearbyint(v);
+  }
+}
+
+int build_informer(cet_engine* e) {
+  const auto& c = e->icfg;
+  const int D = c.d_model;
+  auto& wb = e->wblob;
+  auto& pb = e->pblob;
+  wb.clear();
+  pb.clear();
+  Packer pk{wb, pb};
+  InformerPlan& p = e->ip;
+  std::memset(&p, 0, sizeof(p));
+  const bool lsq = c.lsq_bits > 0;
+  const int bits = c.lsq_bits;
+
+  auto lin = [&](const std::string& n) { return e->W(n + ".weight"); };
+  // Linear/conv1x1 (possibly several concatenated along the output axis) → GemmDesc
+  auto dense = [&](std::vector<std::string> names, int K, bool conv1x1) -> GemmDesc {
+    std::vector<float> w, b, s;
+    for (auto& n : names) {
+      std::vector<float> wi = lin(n);
+      const int Ni = (int)wi.size() / K;
+      float step = 1.f;
+      if (lsq && e->has(n + ".step_size")) {
+        step = e->scalar(n + ".step_size");
+        lsq_grid(wi, step, bits);
+      }
+      w.insert(w.end(), wi.begin(), wi.end());
+      const auto& bi = e->W(n + ".bias");
+      b.insert(b.end(), bi.begin(), bi.end());
+      s.insert(s.end(), Ni, step);
+    }
+    (void)conv1x1;
+    const int N = (int)w.size() / K;
+    return pk.gemm(w, N, K, b.data(), lsq ? s.data() : nullptr);
+  };
+
+  p.C = c.enc_in;
+  p.c_out = c.c_out;
+  p.seq_len = c.seq_len;
+  p.dec_len = c.label_len + c.out_len;
+  p.pred_len = c.out_len;
+  p.n_enc = c.n_enc;
+  p.d_layers = c.d_layers;
+  p.dff = c.d_ff;
+  p.prob = c.attn_prob;
+  p.act_relu = c.act_relu;
+  p.mix = c.mix;
+  p.lsq = lsq;
+
+  // token embeddings: W[n][tap·C + c] = conv.weight[n][c][tap]   (embed.py:30-49)
+  auto emb = [&](const std::string& pre, int C) {
+    const auto& w = e->W(pre + ".value_embedding.tokenConv.weight");
+    std::vector<float> m((size_t)D * 3 * C);
+    for (int n = 0; n < D; ++n)
+      for (int ch = 0; ch < C; ++ch)
+        for (int tap = 0; tap < 3; ++tap) m[(size_t)n * 3 * C + tap * C + ch] = w[((size_t)n * C + ch) * 3 + tap];
+    const auto& b = e->W(pre + ".value_embedding.tokenConv.bias");
+    return pk.gemm(m, D, 3 * C, b.data(), nullptr);
+  };
+  p.emb_enc = emb("enc_embedding", c.enc_in);
+  p.emb_dec = emb("dec_embedding", c.dec_in);
+  {
+    const auto& pe = e->W("enc_embedding.position_embedding.pe");
+    p.pe_enc = pk.vec(pe.data(), LMAX * D, LMAX * D);
+    const auto& pd = e->W("dec_embedding.position_embedding.pe");
+    p.pe_dec = pk.vec(pd.data(), LMAX * D, LMAX * D);
+  }
+
+  int layer = 0, call = 0;
+  int64_t dbg = 0;
+  std::ostringstream js;
+  js << "{\"stages\": [";
+  bool firstj = true;
+  auto jstage = [&](const std::string& name, int64_t off, int rows, int cols) {
+    js << (firstj ? "" : ", ") << "[\"" << name << "\", " << off << ", " << rows << ", " << cols << "]";
+    firstj = false;
+  };
+  p.dbg_emb = (int)dbg;
+  jstage("enc_emb", dbg, c.seq_len, D);
+  dbg += (int64_t)c.seq_len * D;
+  e->calls.clear();
+  e->attn_layout.clear();
+  int64_t attn_off = 0;
+  int S = 0;
+  for (int i = 0; i < c.n_enc; ++i) {
+    const std::string pre = c.stack ? "encoder.encoders." + std::to_string(i) : std::string("encoder");
+    int L = c.stack ? (c.seq_len >> i) : c.seq_len;
+    p.enc_layers[i] = c.e_layers[i];
+    p.enc_first[i] = layer;
+    for (int l = 0; l < c.e_layers[i]; ++l) {
+      if (layer >= MAX_ENC_LAYERS) return fail(CET_E_INVALID, "too many encoder layers");
+      EncLayerDesc& d = p.enc[layer];
+      const std::string lp = pre + ".attn_layers." + std::to_string(l);
+      d.qkv = dense({lp + ".attention.query_projection", lp + ".attention.key_projection",
+                     lp + ".attention.value_projection"}, D, false);
+      d.o = dense({lp + ".attention.out_projection"}, D, false);
+      d.f1 = dense({lp + ".conv1"}, D, true);
+      d.f2 = dense({lp + ".conv2"}, c.d_ff, true);
+      d.ln1 = pk.ln(e->W(lp + ".norm1.weight"), e->W(lp + ".norm1.bias"));
+      d.ln2 = pk.ln(e->W(lp + ".norm2.weight"), e->W(lp + ".norm2.bias"));
+      d.L_in = L;
+      d.call = -1;
+      if (c.attn_prob) {
+        if (call >= MAX_CALLS) return fail(CET_E_INVALID, "too many ProbSparse calls");
+        d.call = call++;
+        e->calls.push_back({L, L, u_part(c.factor, L)});
+      }
+      d.attn_off = (uint32_t)attn_off;
+      if (c.output_attention) {
+        e->attn_layout.push_back({attn_off, L});
+        attn_off += (int64_t)NHEAD * L * L;
+      }
+      d.dbg_layer = (int)dbg;
+      jstage("enc" + std::to_string(i) + "_layer" + std::to_string(l), dbg, L, D);
+      dbg += (int64_t)L * D;
+      d.dbg_conv = -1;
+      d.conv.n = 0;
+      if (c.distil && l < c.e_layers[i] - 1) {
+        // ConvLayer: W[n][tap·D + c] = downConv.weight[n][c][tap]; BatchNorm(eval) folded into
+        // a per-channel scale/shift applied after the conv (encoder.py:22-28).
+        const std::string cp = pre + ".conv_layers." + std::to_string(l);
+        std::vector<float> w = e->W(cp + ".downConv.weight");
+        float step = 1.f;
+        if (lsq && e->has(cp + ".downConv.step_size")) {
+          step = e->scalar(cp + ".downConv.step_size");
+          lsq_grid(w, step, bits);
+        }
+        std::vector<float> m((size_t)D * 3 * D);
+        for (int n = 0; n < D; ++n)
+          for (int ch = 0; ch < D; ++ch)
+            for (int tap = 0; tap < 3; ++tap) m[(size_t)n * 3 * D + tap * D + ch] = w[((size_t)n * D + ch) * 3 + tap];
+        const auto& cb = e->W(cp + ".downConv.bias");
+        const auto& g = e->W(cp + ".norm.weight");
+        const auto& bb = e->W(cp + ".norm.bias");
+        const auto& rm = e->W(cp + ".norm.running_mean");
+        const auto& rv = e->W(cp + ".norm.running_var");
+        std::vector<float> sc(D), sh(D);
+        for (int n = 0; n < D; ++n) {
+          const double inv = (double)g[n] / std::sqrt((double)rv[n] + 1e-5);
+          sc[n] = (float)(inv * step);
+          sh[n] = (float)(((double)cb[n] - rm[n]) * inv + bb[n]);
+        }
+        d.conv = pk.gemm(m, D, 3 * D, sh.data(), sc.data());
+        d.L_out = (L - 1) / 2 + 1;
+        d.dbg_conv = (int)dbg;
+        jstage("enc" + std::to_string(i) + "_conv" + std::to_string(l), dbg, d.L_out, D);
+        dbg += (int64_t)d.L_out * D;
+        L = d.L_out;
+      } else {
+        d.L_out = L;
+      }
+      ++layer;
+    }
+    p.enc_norm[i] = pk.ln(e->W(pre + ".norm.weight"), e->W(pre + ".norm.bias"));
+    p.enc_rows[i] = L;
+    p.enc_row_off[i] = S;
+    S += L;
+    p.enc_dbg[i] = (int)dbg;
+    jstage("enc" + std::to_string(i) + "_out", dbg, L, D);
+    dbg += (int64_t)L * D;
+  }
+  p.S = S;
+  const int Ld = c.label_len + c.out_len;
+  p.dbg_dec_emb = (int)dbg;
+  jstage("dec_emb", dbg, Ld, D);
+  dbg += (int64_t)Ld * D;
+  for (int l = 0; l < c.d_layers; ++l) {
+    DecLayerDesc& d = p.dec[l];
+    const std::string lp = "decoder.layers." + std::to_string(l);
+    d.qkv = dense({lp + ".self_attention.query_projection", lp + ".self_attention.key_projection",
+                   lp + ".self_attention.value_projection"}, D, false);
+    d.o = dense({lp + ".self_attention.out_projection"}, D, false);
+    d.cq = dense({lp + ".cross_attention.query_projection"}, D, false);
+    d.ckv = dense({lp + ".cross_attention.key_projection", lp + ".cross_attention.value_projection"}, D, false);
+    d.co = dense({lp + ".cross_attention.out_projection"}, D, false);
+    d.f1 = dense({lp + ".conv1"}, D, true);
+    d.f2 = dense({lp + ".conv2"}, c.d_ff, true);
+    d.ln1 = pk.ln(e->W(lp + ".norm1.weight"), e->W(lp + ".norm1.bias"));
+    d.ln2 = pk.ln(e->W(lp + ".norm2.weight"), e->W(lp + ".norm2.bias"));
+    d.ln3 = pk.ln(e->W(lp + ".norm3.weight"), e->W(lp + ".norm3.bias"));
+    d.call = -1;
+    if (c.attn_prob) {
+      d.call = call++;
+      e->calls.push_back({Ld, Ld, u_part(c.factor, Ld)});
+    }
+    d.dbg = (int)dbg;
+    jstage("dec_layer" + std::to_string(l), dbg, Ld, D);
+    dbg += (int64_t)Ld * D;
+  }
+  p.dec_norm = pk.ln(e->W("decoder.norm.weight"), e->W("decoder.norm.bias"));
+  p.dbg_dec_out = (int)dbg;
+  jstage("dec_out", dbg, Ld, D);
+  dbg += (int64_t)Ld * D;
+  {
+    const auto& w = e->W("projection.weight");
+    const auto& b = e->W("projection.bias");
+    p.proj = pk.gemm(w, c.c_out, D, b.data(), nullptr);
+  }
+
+  // ProbSparse calls: multiplicity table layout + M debug dumps
+  p.n_calls = (int)e->calls.size();
+  uint32_t coff = 0;
+  js << "], \"m\": [";
+  for (int k = 0; k < p.n_calls; ++k) {
+    AttnCall& ac = p.calls[k];
+    ac.LQ = e->calls[k].LQ;
+    ac.LK = e->calls[k].LK;
+    ac.U = e->calls[k].U;
+    ac.u = u_part(c.factor, ac.LQ);
+    ac.cnt_stride = r16(ac.LK);
+    ac.cnt_off = coff;
+    coff += (uint32_t)(r16(ac.LQ) * ac.cnt_stride);
+    coff = (coff + 15) & ~15u;
+    ac.m_dbg = (int)dbg;
+    js << (k ? ", " : "") << "[" << dbg << ", " << NHEAD << ", " << ac.LQ << "]";
+    dbg += (int64_t)NHEAD * ac.LQ;
+  }
+  js << "]}";
+  p.cnt_bytes = coff;
+  e->cnt_bytes = coff ? coff : 16;
+  p.dbg_stride = (int)dbg;
+  e->dbg_json = js.str();
+  e->attn_floats = attn_off;
+  for (int k = 0; k < MAX_ENC_LAYERS; ++k) p.enc[k].attn_stride = (int)attn_off;
+
+  // LDS layout
+  const int LP = r16(std::max(c.seq_len, Ld));
+  const int SP = r16(S);
+  auto al = [](int x) { return (x + 15) & ~15; };
+  int o = 0;
+  p.lds_X = o; o = al(o + LP * XS * 4);
+  p.lds_Q = o; o = al(o + LP * BS * 2);
+  p.lds_K = o; o = al(o + LP * BS * 2);
+  p.vts = std::max(LP, SP) + 8;
+  p.lds_VT = o; o = al(o + DMODEL * p.vts * 2);
+  p.lds_ENC = o; o = al(o + SP * BS * 2);
+  p.lds_CTX = o; o = al(o + r16(Ld) * BS * 2);
+  p.lds_M = o; o = al(o + NHEAD * 96 * 4);
+  p.lds_SEL = o; o = al(o + NHEAD * 96 * 2);
+  p.lds_FLAG = o; o = al(o + NHEAD * 96);
+  p.lds_bytes = o;
+  p.in_stride = c.enc_in + 4;
+  return CET_OK;
+}
+
+int build_transformer(cet_engine* e);
+
+int check_informer_config(const cet_informer_config& c) {
+  if (c.d_model != DMODEL || c.n_heads != NHEAD)
+    return fail(CET_E_INVALID, "this build supports d_model=128, n_heads=8 (head dim 16)");
+  if (c.enc_in != c.dec_in || (c.enc_in % 8) || c.enc_in > 21)
+    return fail(CET_E_INVALID, "enc_in == dec_in, a multiple of 8, <= 21 required");
+  if (c.d_ff != 64 && c.d_ff != 128) return fail(CET_E_INVALID, "d_ff must be 64 or 128 in this build");
+  if (c.seq_len < 2 || c.seq_len > LMAX) return fail(CET_E_INVALID, "seq_len must be in [2, 96]");
+  const int Ld = c.label_len + c.out_len;
+  if (Ld < 1 || Ld > 48 || c.out_len < 1 || c.out_len > Ld) return fail(CET_E_INVALID, "label_len+out_len must be in [1, 48]");
+  if (c.n_enc < 1 || c.n_enc > MAX_ENC) return fail(CET_E_INVALID, "1..4 encoders");
+  if (!c.stack && c.n_enc != 1) return fail(CET_E_INVALID, "Informer has one encoder");
+  int S = 0, layers = 0;
+  for (int i = 0; i < c.n_enc; ++i) {
+    if (c.e_layers[i] < 1) return fail(CET_E_INVALID, "e_layers entries must be >= 1");
+    int L = c.stack ? (c.seq_len >> i) : c.seq_len;
+    if (L < 1) return fail(CET_E_INVALID, "encoder window is empty");
+    layers += c.e_layers[i];
+    for (int l = 0; l < c.e_layers[i] - 1; ++l)
+      if (c.distil) L = (L - 1) / 2 + 1;
+    S += L;
+  }
+  if (layers > MAX_ENC_LAYERS) return fail(CET_E_INVALID, "too many encoder layers");
+  if (S > LMAX) return fail(CET_E_INVALID, "encoder stack output longer than 96 rows");
+  if (c.d_layers < 1 || c.d_layers > MAX_DEC_LAYERS) return fail(CET_E_INVALID, "1..8 decoder layers");
+  if (c.c_out < 1 || c.c_out > 128) return fail(CET_E_INVALID, "c_out must be in [1, 128]");
+  if (c.factor < 1) return fail(CET_E_INVALID, "factor must be >= 1");
+  if (c.lsq_bits < 0 || c.lsq_bits > 9) return fail(CET_E_INVALID, "lsq_bits must be 0 or 2..9");
+  return CET_OK;
+}
+
+int upload(cet_engine* e) {
+  const void* plan = e->kind == 0 ? (const void*)&e->ip : (const void*)&e->tp;
+  const size_t plan_bytes = e->kind == 0 ? sizeof(InformerPlan) : sizeof(TransformerPlan);
+  if (!e->d_plan) HIP_TRY(hipMalloc(&e->d_plan, sizeof(InformerPlan) > sizeof(TransformerPlan)
+                                                  ? sizeof(InformerPlan) : sizeof(TransformerPlan)));
+  HIP_TRY(hipMemcpy(e->d_plan, plan, plan_bytes, hipMemcpyHostToDevice));
+  const size_t wbytes = e->wblob.size() * 2, pbytes = e->pblob.size() * 4;
+  if (wbytes > e->d_w_bytes) {
+    if (e->d_w) HIP_TRY(hipFree(e->d_w));
+    HIP_TRY(hipMalloc(&e->d_w, wbytes));
+    e->d_w_bytes = wbytes;
+  }
+  if (pbytes > e->d_p_bytes) {
+    if (e->d_p) HIP_TRY(hipFree(e->d_p));
+    HIP_TRY(hipMalloc((void**)&e->d_p, pbytes + 64));
+    e->d_p_bytes = pbytes;
+  }
+  HIP_TRY(hipMemcpy(e->d_w, e->wblob.data(), wbytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_p, e->pblob.data(), pbytes, hipMemcpyHostToDevice));
+  if (e->kind == 0) {
+    for (int i = 0; i < cet_engine::NSLOT; ++i) {
+      if (e->h_cnt[i]) HIP_TRY(hipHostFree(e->h_cnt[i]));
+      if (e->d_cnt[i]) HIP_TRY(hipFree(e->d_cnt[i]));
+      HIP_TRY(hipHostMalloc((void**)&e->h_cnt[i], e->cnt_bytes));
+      HIP_TRY(hipMalloc((void**)&e->d_cnt[i], e->cnt_bytes));
+      if (!e->ev[i]) HIP_TRY(hipEventCreateWithFlags(&e->ev[i], hipEventDisableTiming));
+      e->ev_used[i] = false;
+    }
+  }
+  return CET_OK;
+}
+
+// Host-side packing + plan (no device needed).
+int finalize_host(cet_engine* e) {
+  if (!e->dirty) return CET_OK;
+  for (auto& n : e->order) {
+    const Weight& w = e->weights[n];
+    if (w.required && !w.loaded) return fail(CET_E_MISSING, "weight not loaded: " + n);
+  }
+  int rc = e->kind == 0 ? build_informer(e) : build_transformer(e);
+  if (rc) return rc;
+  e->dirty = false;
+  e->uploaded = false;
+  return CET_OK;
+}
+
+int finalize(cet_engine* e) {
+  int rc = finalize_host(e);
+  if (rc) return rc;
+  if (e->uploaded) return CET_OK;
+  rc = upload(e);
+  if (rc) return rc;
+  e->uploaded = true;
+  return CET_OK;
+}
+
+int build_transformer(cet_engine* e) {
+  const auto& c = e->tcfg;
+  const int D = c.d_model;
+  e->wblob.clear();
+  e->pblob.clear();
+  Packer pk{e->wblob, e->pblob};
+  TransformerPlan& p = e->tp;
+  std::memset(&p, 0, sizeof(p));
+  p.C = c.src_vocab;
+  p.c_out = c.tgt_vocab;
+  p.src_len = c.src_seq_len;
+  p.tgt_len = c.tgt_seq_len + c.label_len;
+  p.pred_len = c.tgt_seq_len;
+  p.N = c.N;
+  p.dff = c.d_ff;
+  // bias-free Q/K/V/O (buildingblocks.py:109-113), concatenated along the output axis
+  auto mha = [&](std::vector<std::string> names) {
+    std::vector<float> w;
+    for (auto& n : names) {
+      const auto& wi = e->W(n + ".weight");
+      w.insert(w.end(), wi.begin(), wi.end());
+    }
+    return pk.gemm(w, (int)w.size() / D, D, nullptr, nullptr);
+  };
+  auto lin = [&](const std::string& n, int K) {
+    const auto& w = e->W(n + ".weight");
+    return pk.gemm(w, (int)w.size() / K, K, e->W(n + ".bias").data(), nullptr);
+  };
+  auto lnt = [&](const std::string& n) { return pk.ln(e->W(n + ".alpha"), e->W(n + ".bias")); };
+  auto emb = [&](const std::string& pre, int C) {
+    const auto& w = e->W(pre + ".weight");
+    std::vector<float> m((size_t)D * 3 * C);
+    for (int n = 0; n < D; ++n)
+      for (int ch = 0; ch < C; ++ch)
+        for (int tap = 0; tap < 3; ++tap) m[(size_t)n * 3 * C + tap * C + ch] = w[((size_t)n * C + ch) * 3 + tap];
+    return pk.gemm(m, D, 3 * C, e->W(pre + ".bias").data(), nullptr);
+  };
+  p.emb_src = emb("src_embed.tokenEmbedding", c.src_vocab);
+  p.emb_tgt = emb("tgt_embed.tokenEmbedding", c.tgt_vocab);
+  p.pe_src = pk.vec(e->W("src_pos.pe").data(), p.src_len * D, p.src_len * D);
+  p.pe_tgt = pk.vec(e->W("tgt_pos.pe").data(), p.tgt_len * D, p.tgt_len * D);
+  int64_t dbg = 0;
+  std::ostringstream js;
+  js << "{\"stages\": [";
+  bool firstj = true;
+  auto jstage = [&](const std::string& name, int64_t off, int rows) {
+    js << (firstj ? "" : ", ") << "[\"" << name << "\", " << off << ", " << rows << ", " << D << "]";
+    firstj = false;
+  };
+  p.dbg_emb = (int)dbg;
+  jstage("enc_emb", dbg, p.src_len);
+  dbg += (int64_t)p.src_len * D;
+  for (int l = 0; l < c.N; ++l) {
+    const std::string lp = "encoder.layers." + std::to_string(l);
+    auto& d = p.enc[l];
+    d.qkv = mha({lp + ".self_attention_block.w_q", lp + ".self_attention_block.w_k", lp + ".self_attention_block.w_v"});
+    d.o = mha({lp + ".self_attention_block.w_o"});
+    d.f1 = lin(lp + ".feed_forward_block.linear_1", D);
+    d.f2 = lin(lp + ".feed_forward_block.linear_2", c.d_ff);
+    d.ln0 = lnt(lp + ".residual_connections.0.norm");
+    d.ln1 = lnt(lp + ".residual_connections.1.norm");
+    d.dbg = (int)dbg;
+    jstage("enc_layer" + std::to_string(l), dbg, p.src_len);
+    dbg += (int64_t)p.src_len * D;
+  }
+  p.enc_norm = lnt("encoder.norm");
+  p.dbg_enc_out = (int)dbg;
+  jstage("enc_out", dbg, p.src_len);
+  dbg += (int64_t)p.src_len * D;
+  p.dbg_dec_emb = (int)dbg;
+  jstage("dec_emb", dbg, p.tgt_len);
+  dbg += (int64_t)p.tgt_len * D;
+  for (int l = 0; l < c.N; ++l) {
+    const std::string lp = "decoder.layers." + std::to_string(l);
+    auto& d = p.dec[l];
+    d.qkv = mha({lp + ".self_attention_block.w_q", lp + ".self_attention_block.w_k", lp + ".self_attention_block.w_v"});
+    d.o = mha({lp + ".self_attention_block.w_o"});
+    d.cq = mha({lp + ".cross_attention_block.w_q"});
+    d.ckv = mha({lp + ".cross_attention_block.w_k", lp + ".cross_attention_block.w_v"});
+    d.co = mha({lp + ".cross_attention_block.w_o"});
+    d.f1 = lin(lp + ".feed_forward_block.linear_1", D);
+    d.f2 = lin(lp + ".feed_forward_block.linear_2", c.d_ff);
+    d.ln0 = lnt(lp + ".residual_connections.0.norm");
+    d.ln1 = lnt(lp + ".residual_connections.1.norm");
+    d.ln2 = lnt(lp + ".residual_connections.2.norm");
+    d.dbg = (int)dbg;
+    jstage("dec_layer" + std::to_string(l), dbg, p.tgt_len);
+    dbg += (int64_t)p.tgt_len * D;
+  }
+  p.dec_norm = lnt("decoder.norm");
+  p.dbg_dec_out = (int)dbg;
+  jstage("dec_out", dbg, p.tgt_len);
+  dbg += (int64_t)p.tgt_len * D;
+  p.proj = lin("projection_layer.proj", D);
+  js << "], \"m\": []}";
+  e->dbg_json = js.str();
+  p.dbg_stride = (int)dbg;
+  e->calls.clear();
+  e->attn_floats = 0;
+  e->attn_layout.clear();
+  // LDS: X fp32 | Q | K (+FFN hidden, staged input) | Vt | ENC (= encoder-phase LN output) | decoder LN output
+  const int LP = r16(std::max(p.src_len, p.tgt_len));
+  auto al = [](int x) { return (x + 15) & ~15; };
+  int o = 0;
+  p.lds_X = o; o = al(o + LP * XS * 4);
+  p.lds_Q = o; o = al(o + LP * BS * 2);
+  p.lds_K = o; o = al(o + LP * BS * 2);
+  p.vts = LP + 8;
+  p.lds_VT = o; o = al(o + DMODEL * p.vts * 2);
+  p.lds_ENC = o; o = al(o + LP * BS * 2);
+  p.lds_XN = o; o = al(o + r16(p.tgt_len) * BS * 2);
+  p.lds_bytes = o;
+  p.in_stride = c.src_vocab + 4;
+  if (o > 160 * 1024) return fail(CET_E_INVALID, "sequence too long for the LDS-resident Transformer kernel");
+  return CET_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char* cet_last_error(void) { return g_err.c_str(); }
+int cet_version(void) { return 1; }
+
+int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
+  if (!cfg || !out) return fail(CET_E_INVALID, "null argument");
+  int rc = check_informer_config(*cfg);
+  if (rc) return rc;
+  auto e = std::make_unique<cet_engine>();
+  e->kind = 0;
+  e->icfg = *cfg;
+  schema_informer(e.get());
+  // shapes of the ProbSparse draws are known before weights arrive
+  const auto& c = *cfg;
+  if (c.attn_prob) {
+    for (int i = 0; i < c.n_enc; ++i) {
+      int L = c.stack ? (c.seq_len >> i) : c.seq_len;
+      for (int l = 0; l < c.e_layers[i]; ++l) {
+        e->calls.push_back({L, L, u_part(c.factor, L)});
+        if (c.distil && l < c.e_layers[i] - 1) L = (L - 1) / 2 + 1;
+      }
+    }
+    const int Ld = c.label_len + c.out_len;
+    for (int l = 0; l < c.d_layers; ++l) e->calls.push_back({Ld, Ld, u_part(c.factor, Ld)});
+  }
+  e->idx.assign(e->calls.size(), {});
+  e->idx_set.assign(e->calls.size(), false);
+  *out = e.release();
+  return CET_OK;
+}
+
+int cet_create_transformer(const cet_transformer_config* cfg, cet_engine** out) {
+  if (!cfg || !out) return fail(CET_E_INVALID, "null argument");
+  const auto& c = *cfg;
+  if (c.d_model != DMODEL || c.h != NHEAD) return fail(CET_E_INVALID, "this build supports d_model=128, h=8");
+  if (c.src_vocab != c.tgt_vocab || (c.src_vocab % 8) || c.src_vocab > 21)
+    return fail(CET_E_INVALID, "src_vocab == tgt_vocab, a multiple of 8, <= 21 required");
+  if (c.d_ff != 64 && c.d_ff != 128) return fail(CET_E_INVALID, "d_ff must be 64 or 128 in this build");
+  if (c.src_seq_len < 2 || c.src_seq_len > LMAX) return fail(CET_E_INVALID, "src_seq_len must be in [2, 96]");
+  const int Ld = c.tgt_seq_len + c.label_len;
+  if (c.tgt_seq_len < 1 || Ld > 48) return fail(CET_E_INVALID, "tgt_seq_len+label_len must be <= 48");
+  if (c.N < 1 || c.N > MAX_DEC_LAYERS) return fail(CET_E_INVALID, "N must be in [1, 8]");
+  auto e = std::make_unique<cet_engine>();
+  e->kind = 1;
+  e->tcfg = c;
+  schema_transformer(e.get());
+  *out = e.release();
+  return CET_OK;
+}
+
+void cet_destroy(cet_engine* e) { delete e; }
+
+int cet_load_weight(cet_engine* e, const char* name, const float* data, int64_t numel) {
+  if (!e || !name || (!data && numel)) return fail(CET_E_INVALID, "null argument");
+  auto it = e->weights.find(name);
+  if (it == e->weights.end()) return fail(CET_E_INVALID, std::string("unexpected key: ") + name);
+  int64_t n = 1;
+  for (auto s : it->second.shape) n *= s;
+  if (n != numel) return fail(CET_E_INVALID, std::string("size mismatch for ") + name);
+  it->second.data.assign(data, data + numel);
+  it->second.loaded = true;
+  e->dirty = true;
+  return CET_OK;
+}
+
+int cet_missing_weights(cet_engine* e, char* first_missing, int buflen) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  int n = 0;
+  for (auto& name : e->order) {
+    const Weight& w = e->weights[name];
+    if (w.required && !w.loaded) {
+      if (!n && first_missing && buflen > 0) std::snprintf(first_missing, buflen, "%s", name.c_str());
+      ++n;
+    }
+  }
+  return n;
+}
+
+int cet_prob_calls(cet_engine* e, int* shapes, int max) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  const int n = (int)e->calls.size();
+  for (int i = 0; i < n && i < max && shapes; ++i) {
+    shapes[3 * i] = e->calls[i].LK;
+    shapes[3 * i + 1] = e->calls[i].LQ;
+    shapes[3 * i + 2] = e->calls[i].U;
+  }
+  return n;
+}
+
+int cet_set_prob_indices(cet_engine* e, int call, const int32_t* idx, int L_Q, int U) {
+  if (!e || !idx) return fail(CET_E_INVALID, "null argument");
+  if (call < 0 || call >= (int)e->calls.size()) return fail(CET_E_INVALID, "call out of range");
+  const auto& c = e->calls[call];
+  if (c.LQ != L_Q || c.U != U) return fail(CET_E_INVALID, "index sample shape mismatch");
+  for (int i = 0; i < L_Q * U; ++i)
+    if (idx[i] < 0 || idx[i] >= c.LK) return fail(CET_E_INVALID, "index out of range");
+  e->idx[call].assign(idx, idx + (size_t)L_Q * U);
+  e->idx_set[call] = true;
+  e->native_rng = false;
+  return CET_OK;
+}
+
+int cet_seed(cet_engine* e, uint64_t seed) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  e->rng.seed(seed);
+  e->native_rng = true;
+  return CET_OK;
+}
+
+int64_t cet_native_draw(cet_engine* e, int32_t* out, int64_t n_max) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (!e->native_rng) return fail(CET_E_STATE, "call cet_seed first");
+  int64_t n = 0;
+  for (const auto& c : e->calls) n += (int64_t)c.LQ * c.U;
+  if (!out) return n;
+  if (n_max < n) return fail(CET_E_INVALID, "buffer too small");
+  int64_t k = 0;
+  for (const auto& c : e->calls)
+    for (int i = 0; i < c.LQ * c.U; ++i) out[k++] = (int32_t)(e->rng.next() % (uint32_t)c.LK);
+  return n;
+}
+
+int64_t cet_attns_floats(cet_engine* e) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  int rc = finalize_host(e);
+  if (rc) return rc;
+  return e->attn_floats;
+}
+
+int cet_attns_layout(cet_engine* e, int64_t* offsets, int* lengths, int max) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  int rc = finalize_host(e);
+  if (rc) return rc;
+  const int n = (int)e->attn_layout.size();
+  for (int i = 0; i < n && i < max; ++i) {
+    if (offsets) offsets[i] = e->attn_layout[i].first;
+    if (lengths) lengths[i] = e->attn_layout[i].second;
+  }
+  return n;
+}
+
+int cet_set_debug(cet_engine* e, float* dbg) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  e->dbg = dbg;
+  return CET_OK;
+}
+
+int64_t cet_debug_floats(cet_engine* e) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  int rc = finalize_host(e);
+  if (rc) return rc;
+  return e->kind == 0 ? e->ip.dbg_stride : e->tp.dbg_stride;
+}
+
+int cet_debug_layout(cet_engine* e, char* json, int buflen) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  int rc = finalize_host(e);
+  if (rc) return rc;
+  if (json && buflen > 0) std::snprintf(json, buflen, "%s", e->dbg_json.c_str());
+  return (int)e->dbg_json.size();
+}
+
+int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
+                void* stream) {
+  if (!e || !x_enc || !x_dec || !out) return fail(CET_E_INVALID, "null argument");
+  if (B < 0 || B > (1 << 24)) return fail(CET_E_INVALID, "bad batch size");
+  int rc = finalize(e);
+  if (rc) return rc;
+  if (B == 0) return CET_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (e->kind == 1) {
+    TransformerArgs a;
+    a.plan = (const TransformerPlan*)e->d_plan;
+    a.weights = e->d_w;
+    a.params = e->d_p;
+    a.x_enc = x_enc;
+    a.x_dec = x_dec;
+    a.out = out;
+    a.dbg = e->dbg;
+    a.B = B;
+    rc = cet_launch_transformer(&a, e->tcfg.d_ff, e->tp.lds_bytes, st);
+    if (rc) return fail(CET_E_HIP, std::string("transformer launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return CET_OK;
+  }
+  // ---- this forward's ProbSparse draws → key multiplicity tables
+  const int k = e->slot;
+  e->slot = (e->slot + 1) % cet_engine::NSLOT;
+  if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
+  uint8_t* h = e->h_cnt[k];
+  const InformerPlan& p = e->ip;
+  if (p.n_calls) {
+    std::memset(h, 0, e->cnt_bytes);
+    for (int c = 0; c < p.n_calls; ++c) {
+      const auto& sh = e->calls[c];
+      const AttnCall& ac = p.calls[c];
+      uint8_t* tab = h + ac.cnt_off;
+      if (e->native_rng) {
+        for (int q = 0; q < sh.LQ; ++q)
+          for (int j = 0; j < sh.U; ++j) tab[q * ac.cnt_stride + (int)(e->rng.next() % (uint32_t)sh.LK)]++;
+      } else {
+        if (!e->idx_set[c]) return fail(CET_E_STATE, "ProbSparse indices not set for call " + std::to_string(c));
+        const int32_t* id = e->idx[c].data();
+        for (int q = 0; q < sh.LQ; ++q)
+          for (int j = 0; j < sh.U; ++j) tab[q * ac.cnt_stride + id[q * sh.U + j]]++;
+      }
+    }
+    if (!e->native_rng) e->idx_set.assign(e->calls.size(), false);
+    HIP_TRY(hipMemcpyAsync(e->d_cnt[k], h, e->cnt_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(e->ev[k], st));
+    e->ev_used[k] = true;
+  }
+  InformerArgs a;
+  a.plan = (const InformerPlan*)e->d_plan;
+  a.weights = e->d_w;
+  a.params = e->d_p;
+  a.cnt = e->d_cnt[k];
+  a.x_enc = x_enc;
+  a.x_dec = x_dec;
+  a.out = out;
+  a.attns = (attns && e->icfg.output_attention) ? attns : nullptr;
+  a.dbg = e->dbg;
+  a.B = B;
+  rc = cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
+  if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
+  return CET_OK;
+}
+
+int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, float* out, int accumulate,
+                   void* stream) {
+  if (!pred || !label || !out) return fail(CET_E_INVALID, "null argument");
+  if (B <= 0 || T <= 0 || F <= 0 || T > 1024) return fail(CET_E_INVALID, "bad shape");
+  int rc = cet_launch_nmse_split(pred, label, B, T, F, out, nullptr, accumulate, (hipStream_t)stream);
+  if (rc) return fail(CET_E_HIP, "nmse launch failed");
+  return CET_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+// Execution plans shared by the host runtime (cet_api.cpp) and the fused kernels.
+// A plan is built once per engine on the host (shapes, weight offsets, LDS layout) and
+// copied to device memory; the kernels read it through scalar loads.
+#pragma once
+#include <stdint.h>
+
+namespace cet {
+
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr int MAX_ENC = 4;
+constexpr int MAX_ENC_LAYERS = 16;   // summed over the encoders of a stack
+constexpr int MAX_DEC_LAYERS = 8;
+constexpr int MAX_CALLS = MAX_ENC_LAYERS + MAX_DEC_LAYERS;
+constexpr int LMAX = 96;             // longest (padded) sequence a workgroup keeps in LDS
+constexpr int DMODEL = 128;
+constexpr int NHEAD = 8;
+constexpr int XS = 132;   // fp32 row stride (floats) of X-like LDS buffers (+16 B per row)
+constexpr int BS = 136;   // bf16 row stride (elements) of Q/K/ctx-like LDS buffers (+16 B per row)
+
+// One dense layer: packed bf16 weights (fragment order) + fp32 epilogue vectors.
+struct GemmDesc {
+  uint32_t w;      // offset into the weight blob, in bf16x8 (16-byte) units
+  uint32_t bias;   // float offset into the parameter blob (NONE: no bias)
+  uint32_t scale;  // float offset of a per-output scale (NONE: 1.0) — LSQ step / BatchNorm fold
+  uint16_t n;      // output features (padded to 16)
+  uint16_t k;      // input features (padded to 32)
+};
+
+struct LNDesc {
+  uint32_t g, b;   // float offsets of gamma / beta
+};
+
+struct EncLayerDesc {
+  GemmDesc qkv, o, f1, f2;
+  LNDesc ln1, ln2;
+  GemmDesc conv;         // distil ConvLayer following this layer (n == 0: none)
+  int L_in, L_out;       // rows entering the layer / leaving its ConvLayer
+  int call;              // index into calls[] (ProbSparse) or -1
+  uint32_t attn_off;     // float offset of this layer's attns map in the attns buffer (per batch 0)
+  int attn_stride;       // floats per batch element of that map (H·L·L)
+  int dbg_layer, dbg_conv;  // debug-dump float offsets (per sequence), -1: none
+};
+
+struct DecLayerDesc {
+  GemmDesc qkv, o, cq, ckv, co, f1, f2;
+  LNDesc ln1, ln2, ln3;
+  int call;
+  int dbg;
+};
+
+struct AttnCall {
+  int LQ, LK, U, u;
+  uint32_t cnt_off;      // byte offset into the per-forward multiplicity blob
+  int cnt_stride;        // bytes per query row
+  int m_dbg;             // debug float offset of M [H][LQ], -1: none
+};
+
+struct InformerPlan {
+  int C, c_out, seq_len, dec_len, pred_len;
+  int n_enc;
+  int enc_layers[MAX_ENC];
+  int enc_first[MAX_ENC];   // index of the encoder's first layer in enc[]
+  int enc_rows[MAX_ENC];    // output rows of each encoder
+  int enc_row_off[MAX_ENC]; // row offset of each encoder's output in the concatenated stack output
+  int enc_dbg[MAX_ENC];
+  int d_layers, dff, prob, act_relu, mix, lsq;
+  int S;                    // total encoder output rows (cross-attention keys)
+  GemmDesc emb_enc, emb_dec, proj;
+  uint32_t pe_enc, pe_dec;  // float offsets of the positional tables [LMAX][128]
+  EncLayerDesc enc[MAX_ENC_LAYERS];
+  LNDesc enc_norm[MAX_ENC];
+  DecLayerDesc dec[MAX_DEC_LAYERS];
+  LNDesc dec_norm;
+  AttnCall calls[MAX_CALLS];
+  int n_calls;
+  uint32_t cnt_bytes;
+  // LDS layout (byte offsets) and size
+  int lds_X, lds_Q, lds_K, lds_VT, lds_ENC, lds_CTX, lds_M, lds_SEL, lds_FLAG, lds_bytes;
+  int vts;
+  int in_stride;            // floats per staged input row
+  int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
+};
+
+struct TransformerPlan {
+  int C, c_out, src_len, tgt_len, pred_len, N, dff;
+  GemmDesc emb_src, emb_tgt, proj;
+  uint32_t pe_src, pe_tgt;
+  struct Enc { GemmDesc qkv, o, f1, f2; LNDesc ln0, ln1; int dbg; } enc[MAX_DEC_LAYERS];
+  struct Dec { GemmDesc qkv, o, cq, ckv, co, f1, f2; LNDesc ln0, ln1, ln2; int dbg; } dec[MAX_DEC_LAYERS];
+  LNDesc enc_norm, dec_norm;
+  int lds_X, lds_XN, lds_Q, lds_K, lds_VT, lds_ENC, lds_bytes;
+  int vts;
+  int in_stride;
+  int dbg_stride, dbg_emb, dbg_enc_out, dbg_dec_emb, dbg_dec_out;
+};
+
+}  // namespace cet

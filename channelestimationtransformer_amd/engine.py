@@ -1,0 +1,156 @@
+"""Thin object wrapper over one C-ABI engine handle (include/cet.h).
+
+torch is used only as plumbing: device buffers, the current HIP stream, and the
+global CPU generator for the reference's ProbSparse RNG protocol.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _stream_ptr(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Engine:
+    """Owns a ``cet_engine*``; weights by reference key name; forward on device tensors."""
+
+    def __init__(self, handle: int, kind: str):
+        self._h = ctypes.c_void_p(handle)
+        self.kind = kind
+        self._dbg = None
+
+    @classmethod
+    def informer(cls, cfg: "_lib.InformerConfig") -> "Engine":
+        h = ctypes.c_void_p()
+        check(lib.cet_create_informer(ctypes.byref(cfg), ctypes.byref(h)), "cet_create_informer")
+        return cls(h.value, "informer")
+
+    @classmethod
+    def transformer(cls, cfg: "_lib.TransformerConfig") -> "Engine":
+        h = ctypes.c_void_p()
+        check(lib.cet_create_transformer(ctypes.byref(cfg), ctypes.byref(h)), "cet_create_transformer")
+        return cls(h.value, "transformer")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.cet_destroy(h)
+            self._h = ctypes.c_void_p()
+
+    # ------------------------------------------------------------------ weights
+    def load_state_dict(self, state: Mapping[str, object], strict: bool = False) -> List[str]:
+        """Push every tensor of ``state`` (reference key names).  Unknown keys raise if strict."""
+        unexpected = []
+        for k, v in state.items():
+            a = np.ascontiguousarray(_to_numpy(v), dtype=np.float32)
+            rc = lib.cet_load_weight(self._h, k.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size)
+            if rc < 0:
+                if strict or "size mismatch" in lib.cet_last_error().decode():
+                    check(rc, f"load {k}")
+                unexpected.append(k)
+        return unexpected
+
+    def missing(self) -> Tuple[int, str]:
+        buf = ctypes.create_string_buffer(512)
+        n = check(lib.cet_missing_weights(self._h, buf, 512), "cet_missing_weights")
+        return n, buf.value.decode()
+
+    # ------------------------------------------------------------------ ProbSparse sampling
+    def prob_calls(self) -> List[Tuple[int, Tuple[int, int]]]:
+        n = check(lib.cet_prob_calls(self._h, None, 0))
+        arr = (ctypes.c_int * (3 * max(n, 1)))()
+        check(lib.cet_prob_calls(self._h, arr, n))
+        return [(arr[3 * i], (arr[3 * i + 1], arr[3 * i + 2])) for i in range(n)]
+
+    def set_indices(self, idx: Sequence[np.ndarray]) -> None:
+        for k, a in enumerate(idx):
+            a = np.ascontiguousarray(a, dtype=np.int32)
+            check(lib.cet_set_prob_indices(self._h, k, a.ctypes.data_as(ctypes.c_void_p), a.shape[0], a.shape[1]),
+                  "cet_set_prob_indices")
+
+    def native_draw(self) -> List[np.ndarray]:
+        """Next forward's draws from the native sampler (advances it), split per call."""
+        n = check(lib.cet_native_draw(self._h, None, 0), "cet_native_draw")
+        buf = np.empty(max(n, 1), dtype=np.int32)
+        check(lib.cet_native_draw(self._h, buf.ctypes.data_as(ctypes.c_void_p), n), "cet_native_draw")
+        out, k = [], 0
+        for _, (lq, u) in self.prob_calls():
+            out.append(buf[k:k + lq * u].reshape(lq, u))
+            k += lq * u
+        return out
+
+    def seed(self, seed: int) -> None:
+        check(lib.cet_seed(self._h, ctypes.c_uint64(int(seed) & (2 ** 64 - 1))), "cet_seed")
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x_enc, x_dec, out, attns=None, stream: Optional[int] = None) -> None:
+        """All arguments are contiguous float32 torch tensors on the same HIP device."""
+        B = int(x_enc.shape[0])
+        if stream is None:
+            stream = _stream_ptr(x_enc.device)
+        check(lib.cet_forward(self._h, ctypes.c_void_p(x_enc.data_ptr()), ctypes.c_void_p(x_dec.data_ptr()), B,
+                              ctypes.c_void_p(out.data_ptr()),
+                              ctypes.c_void_p(attns.data_ptr()) if attns is not None else None,
+                              ctypes.c_void_p(stream)), "cet_forward")
+
+    def attns_floats(self) -> int:
+        return check(lib.cet_attns_floats(self._h), "cet_attns_floats")
+
+    def attns_layout(self) -> List[Tuple[int, int]]:
+        n = check(lib.cet_attns_layout(self._h, None, None, 0))
+        offs = (ctypes.c_int64 * max(n, 1))()
+        lens = (ctypes.c_int * max(n, 1))()
+        check(lib.cet_attns_layout(self._h, offs, lens, n))
+        return [(offs[i], lens[i]) for i in range(n)]
+
+    # ------------------------------------------------------------------ debug dumps
+    def debug_floats(self) -> int:
+        return check(lib.cet_debug_floats(self._h), "cet_debug_floats")
+
+    def debug_layout(self) -> dict:
+        n = check(lib.cet_debug_layout(self._h, None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        check(lib.cet_debug_layout(self._h, buf, n + 1))
+        return json.loads(buf.value.decode())
+
+    def set_debug(self, buf) -> None:
+        self._dbg = buf
+        check(lib.cet_set_debug(self._h, ctypes.c_void_p(buf.data_ptr()) if buf is not None else None))
+
+
+def nmse_split(pred, label, out=None, accumulate: bool = False, stream: Optional[int] = None):
+    """Device NMSE_Split_cuda(pred, label) → fp32 tensor [T] (FullPrecision/metrics.py:26-30)."""
+    import torch
+
+    B, T, F = pred.shape
+    if out is None:
+        out = torch.zeros(T, dtype=torch.float32, device=pred.device)
+    if stream is None:
+        stream = _stream_ptr(pred.device)
+    check(lib.cet_nmse_split(ctypes.c_void_p(pred.data_ptr()), ctypes.c_void_p(label.data_ptr()), B, T, F,
+                             ctypes.c_void_p(out.data_ptr()), int(accumulate), ctypes.c_void_p(stream)),
+          "cet_nmse_split")
+    return out
+
+
+def _to_numpy(v):
+    if isinstance(v, np.ndarray):
+        return v
+    try:
+        import torch
+
+        if isinstance(v, torch.Tensor):
+            return v.detach().to("cpu", torch.float32).numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    return np.asarray(v)

@@ -1,0 +1,264 @@
+"""Drop-in ``InformerStack`` / ``Informer`` whose forward runs on the HIP engine.
+
+Same constructor signature and positional order as the reference
+(``FullPrecision/InformerModel/model.py:11-31`` / ``:142-166``), same state_dict keys
+(:mod:`.spec`), same ``forward(x_enc, x_mark_enc, x_dec, x_mark_dec, ...)`` and the
+same return convention (``(out, attns)`` when ``output_attention`` else ``out``,
+``model.py:268-271``).  The module only holds the parameters; every forward goes
+through ``libcet.so`` (no CPU/PyTorch fallback exists).
+
+Flags are resolved exactly as the reference resolves them, including the callers'
+positional shift: the 19-argument call of
+``QuantizationAwareTraining.py:63-83`` puts ``activation`` in ``freq``,
+``output_attention`` in ``activation`` (→ GELU, since it is not "relu",
+``encoder.py:41``), ``distil`` in ``output_attention`` and the device in ``distil``.
+"""
+from __future__ import annotations
+
+from collections.abc import Sequence as _Seq
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import spec as S
+from ._lib import InformerConfig
+from .engine import Engine
+from .rng import draw_indices
+from .weights import synthetic_state_dict
+
+
+def build_param_tree(root: nn.Module, entries, values=None) -> None:
+    """Create nested sub-modules so that ``root.state_dict()`` has exactly the schema's keys."""
+    for key, shape, kind in entries:
+        *path, leaf = key.split(".")
+        mod = root
+        for p in path:
+            if not hasattr(mod, p) or not isinstance(getattr(mod, p), nn.Module):
+                mod.add_module(p, nn.Module())
+            mod = getattr(mod, p)
+        if values is not None and key in values:
+            t = torch.as_tensor(np.asarray(values[key]))
+        else:
+            t = torch.zeros(shape, dtype=torch.int64 if kind == "bn_nbt" else torch.float32)
+        if kind in ("pe", "bn_rm", "bn_rv", "bn_nbt"):
+            mod.register_buffer(leaf, t.clone())
+        else:
+            mod.register_parameter(leaf, nn.Parameter(t.clone(), requires_grad=False))
+
+
+class _EngineModule(nn.Module):
+    """Parameter container + lazily (re)built engine bound to one HIP device."""
+
+    def __init__(self):
+        super().__init__()
+        self._engine: Optional[Engine] = None
+        self._engine_device = None
+        self._synced_version = None
+        self.native_rng_seed: Optional[int] = None   # None: draw from torch's global generator
+
+    def _make_engine(self) -> Engine:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def _version(self):
+        return tuple(t._version for t in self.state_dict().values()) + (id(self),)
+
+    def engine(self, device) -> Engine:
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("the engine runs on a HIP device only (no CPU fallback); move inputs to cuda")
+        if self._engine is None or self._engine_device != device:
+            with torch.cuda.device(device):
+                self._engine = self._make_engine()
+            self._engine_device = device
+            self._synced_version = None
+        v = self._version()
+        if v != self._synced_version:
+            self._engine.load_state_dict(self.state_dict())
+            n, first = self._engine.missing()
+            if n:
+                raise RuntimeError(f"{n} weights missing, first: {first}")
+            self._synced_version = v
+        return self._engine
+
+    def refresh(self):
+        """Force re-packing of the weights at the next forward."""
+        self._synced_version = None
+
+    def train(self, mode: bool = True):
+        return super().train(mode)
+
+
+class LazyAttns(_Seq):
+    """The ``attns`` return value: per encoder, per layer ``[B, H, L, L]`` maps.
+
+    Materialising them costs ~346 KB of HBM writes per sequence, so they are
+    produced only when first indexed, by replaying the same forward (same inputs, same
+    ProbSparse draws) with the attention-map output enabled.
+    """
+
+    def __init__(self, producer, n_enc, layers_per_enc, stack):
+        self._producer = producer
+        self._n_enc = n_enc
+        self._layers = layers_per_enc
+        self._stack = stack
+        self._val = None
+
+    def _get(self):
+        if self._val is None:
+            flat = self._producer()
+            out, k = [], 0
+            for n in self._layers:
+                out.append(flat[k:k + n])
+                k += n
+            self._val = out if self._stack else out[0]
+            self._producer = None
+        return self._val
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __len__(self):
+        return self._n_enc if self._stack else self._layers[0]
+
+
+class InformerStack(_EngineModule):
+    """``InformerStack`` (model.py:142-271) on the MI355X engine."""
+
+    _stack = True
+
+    def __init__(self, enc_in, dec_in, c_out, seq_len, label_len, out_len, factor=5, d_model=512, n_heads=8,
+                 e_layers=[3, 2, 1], d_layers=2, d_ff=512, dropout=0.0, attn="prob", embed="fixed", freq="h",
+                 activation="gelu", output_attention=False, distil=True, mix=True, device=None):
+        super().__init__()
+        self.pred_len = out_len
+        self.attn = attn
+        self.output_attention = output_attention
+        self.enc_in, self.dec_in, self.c_out = enc_in, dec_in, c_out
+        self.seq_len, self.label_len = seq_len, label_len
+        self.factor, self.d_model, self.n_heads = factor, d_model, n_heads
+        self.e_layers = list(e_layers) if self._stack else [int(e_layers)]
+        self.d_layers, self.d_ff = d_layers, d_ff
+        self.embed, self.freq = embed, freq
+        # encoder.py:41 / decoder.py:26: anything but "relu" selects GELU
+        self.act_relu = activation == "relu"
+        self.distil = bool(distil)
+        self.mix = bool(mix)
+        self.lsq_bits = 0
+        self.materialize_attns = False
+        entries = self._schema()
+        build_param_tree(self, entries, synthetic_state_dict(entries, seed=int(torch.initial_seed()) % (2 ** 32)))
+
+    def _schema(self):
+        if self._stack:
+            return S.informer_stack_spec(self.enc_in, self.dec_in, self.c_out, self.d_model, self.n_heads,
+                                         self.e_layers, self.d_layers, self.d_ff, self.embed, self.freq,
+                                         self.distil, lsq=self.lsq_bits > 0)
+        return S.informer_spec(self.enc_in, self.dec_in, self.c_out, self.d_model, self.n_heads,
+                               self.e_layers[0], self.d_layers, self.d_ff, self.embed, self.freq, self.distil)
+
+    def config(self) -> InformerConfig:
+        c = InformerConfig()
+        c.enc_in, c.dec_in, c.c_out = self.enc_in, self.dec_in, self.c_out
+        c.seq_len, c.label_len, c.out_len = self.seq_len, self.label_len, self.pred_len
+        c.factor, c.d_model, c.n_heads = self.factor, self.d_model, self.n_heads
+        c.n_enc = len(self.e_layers)
+        for i, v in enumerate(self.e_layers[:4]):
+            c.e_layers[i] = v
+        c.d_layers, c.d_ff = self.d_layers, self.d_ff
+        c.attn_prob = int(self.attn == "prob")
+        c.distil, c.mix = int(self.distil), int(self.mix)
+        c.output_attention = int(bool(self.output_attention))
+        c.act_relu = int(self.act_relu)
+        c.stack = int(self._stack)
+        c.lsq_bits = int(self.lsq_bits)
+        return c
+
+    def _make_engine(self) -> Engine:
+        if len(self.e_layers) > 4:
+            raise ValueError("at most 4 encoders in a stack")
+        return Engine.informer(self.config())
+
+    def forward(self, x_enc, x_mark_enc, x_dec, x_mark_dec, enc_self_mask=None, dec_self_mask=None,
+                dec_enc_mask=None):
+        """model.py:247-271.  ``x_mark_*`` and the masks are accepted and ignored, as in the reference
+        (embed.py:132-135; ProbAttention builds its own masks, attn.py:130-132)."""
+        if self.training:
+            raise RuntimeError("inference-only engine: call .eval() first (dropout/BatchNorm train mode "
+                               "is not implemented)")
+        dev = x_enc.device if x_enc.is_cuda else torch.device("cuda", torch.cuda.current_device())
+        eng = self.engine(dev)
+        xe = x_enc.to(dev, torch.float32).contiguous()
+        xd = x_dec.to(dev, torch.float32).contiguous()
+        B = xe.shape[0]
+        if xe.shape[1:] != (self.seq_len, self.enc_in) or xd.shape[1:] != (self.label_len + self.pred_len, self.dec_in):
+            raise ValueError(f"expected x_enc [B,{self.seq_len},{self.enc_in}] and "
+                             f"x_dec [B,{self.label_len + self.pred_len},{self.dec_in}]")
+        idx = None
+        if self.attn == "prob":
+            if self.native_rng_seed is None:
+                idx = draw_indices(eng.prob_calls())       # global generator, reference call order
+                eng.set_indices(idx)
+        out = torch.empty(B, self.pred_len, self.c_out, device=dev, dtype=torch.float32)
+        attn_buf = None
+        if self.output_attention and self.materialize_attns:
+            attn_buf = torch.empty(max(B * eng.attns_floats(), 1), device=dev, dtype=torch.float32)
+        eng.forward(xe, xd, out, attn_buf)
+        if not self.output_attention:
+            return out
+        if attn_buf is not None:
+            return out, self._attn_views(eng, attn_buf, B)
+
+        def produce():
+            buf = torch.empty(max(B * eng.attns_floats(), 1), device=dev, dtype=torch.float32)
+            if idx is not None:
+                eng.set_indices(idx)
+            tmp = torch.empty_like(out)
+            eng.forward(xe, xd, tmp, buf)
+            return self._attn_views(eng, buf, B, flat=True)
+
+        return out, LazyAttns(produce, len(self.e_layers), self.e_layers, self._stack)
+
+    def _attn_views(self, eng, buf, B, flat=False):
+        per = eng.attns_floats()
+        views = [buf.as_strided((B, self.n_heads, L, L), (per, L * L, L, 1), off) for off, L in eng.attns_layout()]
+        if flat:
+            return views
+        out, k = [], 0
+        for n in self.e_layers:
+            out.append(views[k:k + n])
+            k += n
+        return out if self._stack else out[0]
+
+
+class Informer(InformerStack):
+    """Single-encoder ``Informer`` (model.py:11-139); ``e_layers`` is an int."""
+
+    _stack = False
+
+
+class InformerStackLSQ(InformerStack):
+    """``models/InformerLSQ`` InformerStack: LSQ fake-quantised weights (LSQ.py:23-74, 247-314).
+
+    The callers pass ``num_bits`` as a 20th positional argument, which lands in ``mix``
+    (TrainInformerLSQ.py:80-101; truthy, so the decoder keeps its mix scramble), then switch
+    every LinearLSQ/Conv1dLSQ to ``quantize=True`` (:104-116) — :meth:`enable_lsq` here.
+    The engine packs the integer grid ``round(clamp(w/s, Qn, Qp))`` exactly in bf16 and
+    applies the per-tensor step ``s`` in the GEMM epilogue.
+    """
+
+    def enable_lsq(self, nbits: int):
+        """quantize=True, nbits, reset_parameters(): ``s = mean|w| / sqrt(Qp)`` (LSQ.py:54-58)."""
+        from .weights import lsq_step_sizes
+
+        self.lsq_bits = int(nbits)
+        entries = self._schema()
+        cur = {k: v.detach().cpu().numpy() for k, v in self.state_dict().items()}
+        steps = [k for k, _, kind in entries if kind == "step"]
+        cur.update(lsq_step_sizes(cur, steps, nbits=self.lsq_bits))
+        for name in list(dict(self.named_children())):
+            delattr(self, name)
+        build_param_tree(self, entries, cur)
+        self._engine = None
+        return self

@@ -1,0 +1,106 @@
+/* cet.h — C ABI of the MI355X channel-prediction engine (libcet.so).
+ *
+ * Drop-in boundary for the reference's model calls.  Plain pointers and
+ * sizes only; device pointers are HIP device memory, `stream` is a hipStream_t
+ * (NULL = default stream).  Every function returns 0 on success and a negative code
+ * on error; cet_last_error() then describes it (thread-local).  A handle is not
+ * thread-safe; use one handle per host thread / stream.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   cet_create_informer      InformerStack.__init__ / Informer.__init__
+ *                            FullPrecision/InformerModel/model.py:142-245 / :11-113,
+ *                            models/InformerLSQ/model.py (LSQ variant, num_bits)
+ *   cet_create_transformer   build_transformer  models/Transformer/model.py:90-174
+ *   cet_load_weight          nn.Module.load_state_dict (reference key names,
+ *                            e.g. "encoder.encoders.0.attn_layers.0.attention.query_projection.weight")
+ *                            as used at FullPrecision/QuantizationAwareTraining.py:192-202
+ *   cet_set_prob_indices     the torch.randint draw inside ProbAttention._prob_QK
+ *                            FullPrecision/InformerModel/attn.py:96-98 (parity mode)
+ *   cet_seed                 torch.manual_seed + that draw, reproduced natively (mt19937 % L_K)
+ *   cet_forward              InformerStack.forward / Transformer.forward
+ *                            FullPrecision/InformerModel/model.py:247-271,
+ *                            models/Transformer/model.py:76-87
+ *   cet_nmse_split           NMSELossSplit / NMSE_Split_cuda  FullPrecision/metrics.py:26-39
+ */
+#ifndef CET_H
+#define CET_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cet_engine cet_engine;
+
+enum {
+  CET_OK = 0,
+  CET_E_INVALID = -1,     /* bad argument / unsupported configuration */
+  CET_E_MISSING = -2,     /* a required weight was never loaded */
+  CET_E_HIP = -3,         /* HIP runtime error */
+  CET_E_STATE = -4        /* call out of order (e.g. indices not set) */
+};
+
+/* Effective InformerStack flags (after the callers' positional shift). */
+typedef struct {
+  int enc_in, dec_in, c_out;
+  int seq_len, label_len, out_len;
+  int factor, d_model, n_heads;
+  int n_enc;              /* encoders in the stack (len(e_layers)); 1 for Informer */
+  int e_layers[4];
+  int d_layers, d_ff;
+  int attn_prob;          /* 1: attn == "prob", 0: "full" */
+  int distil, mix, output_attention;
+  int act_relu;           /* 1: ReLU FFN, 0: GELU */
+  int stack;              /* 1: InformerStack (EncoderStack windows), 0: Informer */
+  int lsq_bits;           /* 0: full precision; else models/InformerLSQ weight grid */
+} cet_informer_config;
+
+typedef struct {
+  int src_vocab, tgt_vocab, src_seq_len, tgt_seq_len, label_len, d_model, N, h, d_ff;
+} cet_transformer_config;
+
+const char* cet_last_error(void);
+int cet_version(void);
+
+int cet_create_informer(const cet_informer_config* cfg, cet_engine** out);
+int cet_create_transformer(const cet_transformer_config* cfg, cet_engine** out);
+void cet_destroy(cet_engine* e);
+
+/* host fp32 data, `numel` elements, reference state_dict key name */
+int cet_load_weight(cet_engine* e, const char* name, const float* data, int64_t numel);
+/* number of weights the engine still needs (0 when ready) */
+int cet_missing_weights(cet_engine* e, char* first_missing, int buflen);
+
+/* ProbSparse sampling.  cet_prob_calls() returns the number of torch.randint draws one
+ * forward makes; shapes[i*3..] = {L_K, L_Q, U} for i < max. */
+int cet_prob_calls(cet_engine* e, int* shapes, int max);
+int cet_set_prob_indices(cet_engine* e, int call, const int32_t* host_idx, int L_Q, int U);
+int cet_seed(cet_engine* e, uint64_t seed);          /* switch to the native sampler */
+/* Draw one forward's worth of indices (all calls, concatenated, row-major) from the native
+ * sampler into host memory, advancing it exactly as cet_forward would; returns the count
+ * (out == NULL: only the count). */
+int64_t cet_native_draw(cet_engine* e, int32_t* out, int64_t n_max);
+
+/* Forward on device buffers: x_enc [B][seq_len][enc_in], x_dec [B][label_len+out_len][dec_in]
+ * → out [B][out_len][c_out].  attns (optional, Informer with output_attention): per
+ * sequence block of cet_attns_floats() floats; layer views via cet_attns_layout(). */
+int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
+                void* stream);
+int64_t cet_attns_floats(cet_engine* e);
+int cet_attns_layout(cet_engine* e, int64_t* offsets, int* lengths, int max);
+
+/* Debug: per-stage activation dumps into a device buffer of B·cet_debug_floats() floats. */
+int cet_set_debug(cet_engine* e, float* dbg_dev);
+int64_t cet_debug_floats(cet_engine* e);
+int cet_debug_layout(cet_engine* e, char* json, int buflen);
+
+/* NMSE_Split_cuda(x_hat=pred, x=label) per prediction step over [B][T][F] fp32 device
+ * tensors → out_dev[T] (fp32); if accumulate, out_dev[T] += ratio instead of =. */
+int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, float* out_dev, int accumulate,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
