@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int64, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcet.so")
@@ -53,6 +53,8 @@ def _load():
         "cet_debug_floats": (c_int64, [c_void_p]),
         "cet_debug_layout": (c_int, [c_void_p, c_char_p, c_int]),
         "cet_nmse_split": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
+        "cet_timing": (c_int, [c_void_p, c_int]),
+        "cet_timing_read": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -66,7 +68,7 @@ EXPORTED = ("cet_last_error", "cet_version", "cet_create_informer", "cet_create_
             "cet_load_weight", "cet_missing_weights", "cet_prob_calls", "cet_set_prob_indices", "cet_seed",
             "cet_native_draw",
             "cet_forward", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
-            "cet_debug_layout", "cet_nmse_split")
+            "cet_debug_layout", "cet_nmse_split", "cet_timing", "cet_timing_read")
 
 
 def check(rc: int, what: str = "") -> int:

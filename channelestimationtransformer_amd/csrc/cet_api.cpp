@@ -122,10 +122,16 @@ struct cet_engine {
 
   float* dbg = nullptr;
   std::string dbg_json;
+
+  // kernel timing: hipEvents bracketing each forward kernel launch on the caller's stream
+  bool timing = false;
+  std::vector<hipEvent_t> t_ev;
+  size_t t_n = 0;
   int64_t attn_floats = 0;
   std::vector<std::pair<int64_t, int>> attn_layout;  // (offset, L) per encoder layer
 
   ~cet_engine() {
+    for (auto ev_ : t_ev) (void)hipEventDestroy(ev_);
     if (d_plan) (void)hipFree(d_plan);
     if (d_w) (void)hipFree(d_w);
     if (d_p) (void)hipFree(d_p);
@@ -767,6 +773,21 @@ int build_transformer(cet_engine* e) {
   return CET_OK;
 }
 
+// Record the "before" event of a timed launch (returns the pair index, or -1).
+int timing_mark(cet_engine* e, hipStream_t st) {
+  if (!e->timing) return -1;
+  if (e->t_n * 2 + 2 > e->t_ev.size()) {
+    for (int i = 0; i < 64; ++i) {
+      hipEvent_t ev_;
+      if (hipEventCreate(&ev_) != hipSuccess) return -1;
+      e->t_ev.push_back(ev_);
+    }
+  }
+  const int k = (int)e->t_n++;
+  (void)hipEventRecord(e->t_ev[2 * k], st);
+  return k;
+}
+
 }  // namespace
 
 // =================================================================== C ABI
@@ -951,7 +972,9 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     a.out = out;
     a.dbg = e->dbg;
     a.B = B;
+    const int tk = timing_mark(e, st);
     rc = cet_launch_transformer(&a, e->tcfg.d_ff, e->tp.lds_bytes, st);
+    if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
     if (rc) return fail(CET_E_HIP, std::string("transformer launch failed: ") + hipGetErrorString(hipGetLastError()));
     return CET_OK;
   }
@@ -993,8 +1016,31 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.attns = (attns && e->icfg.output_attention) ? attns : nullptr;
   a.dbg = e->dbg;
   a.B = B;
+  const int tk = timing_mark(e, st);
   rc = cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
+  if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
+  return CET_OK;
+}
+
+int cet_timing(cet_engine* e, int enable) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  e->timing = enable != 0;
+  e->t_n = 0;
+  return CET_OK;
+}
+
+int cet_timing_read(cet_engine* e, double* total_ms, int64_t* launches) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  double tot = 0.0;
+  for (size_t k = 0; k < e->t_n; ++k) {
+    HIP_TRY(hipEventSynchronize(e->t_ev[2 * k + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->t_ev[2 * k], e->t_ev[2 * k + 1]));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = (int64_t)e->t_n;
   return CET_OK;
 }
 

@@ -113,6 +113,17 @@ class Engine:
         check(lib.cet_attns_layout(self._h, offs, lens, n))
         return [(offs[i], lens[i]) for i in range(n)]
 
+    # ------------------------------------------------------------------ kernel timing
+    def timing(self, enable: bool) -> None:
+        check(lib.cet_timing(self._h, int(enable)), "cet_timing")
+
+    def timing_read(self) -> Tuple[float, int]:
+        """(summed kernel milliseconds, launches) since ``timing(True)``."""
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(lib.cet_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)), "cet_timing_read")
+        return ms.value, n.value
+
     # ------------------------------------------------------------------ debug dumps
     def debug_floats(self) -> int:
         return check(lib.cet_debug_floats(self._h), "cet_debug_floats")

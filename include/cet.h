@@ -95,6 +95,12 @@ int cet_set_debug(cet_engine* e, float* dbg_dev);
 int64_t cet_debug_floats(cet_engine* e);
 int cet_debug_layout(cet_engine* e, char* json, int buflen);
 
+/* Kernel timing: when enabled, every cet_forward brackets its kernel launch with a pair of
+ * hipEvents on the caller's stream; cet_timing_read() waits for them and returns the summed
+ * kernel time and launch count since cet_timing(e, 1). */
+int cet_timing(cet_engine* e, int enable);
+int cet_timing_read(cet_engine* e, double* total_ms, int64_t* launches);
+
 /* NMSE_Split_cuda(x_hat=pred, x=label) per prediction step over [B][T][F] fp32 device
  * tensors → out_dev[T] (fp32); if accumulate, out_dev[T] += ratio instead of =. */
 int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, float* out_dev, int accumulate,
