@@ -95,6 +95,7 @@ def main():
     ap.add_argument("--snr", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--variant", type=int, default=2, help="fused-kernel generation (1: LDS-resident, 2: register-resident)")
     args = ap.parse_args()
 
     import torch
@@ -119,6 +120,7 @@ def main():
 
     model = build_model(dev)
     eng = model.engine(dev)
+    eng.set_variant(args.variant)
     eng.seed(1)                 # every rank draws the same index samples (shared across the batch)
     B = args.batch
     xe_np, xd_np, lab_np = make_batch(B, snr=args.snr, seed=1234 + 7919 * rank)
@@ -206,7 +208,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                          "traffic": load_traffic(os.path.join(ROOT, "profiles")),
-                         "kernel": "cet::informer_forward<64>", "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel": "cet::v2::informer_forward_v2<64>" if args.variant == 2 else "cet::informer_forward<64>", "kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }

@@ -54,6 +54,8 @@ def _load():
         "cet_debug_layout": (c_int, [c_void_p, c_char_p, c_int]),
         "cet_nmse_split": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
         "cet_timing": (c_int, [c_void_p, c_int]),
+        "cet_set_variant": (c_int, [c_void_p, c_int]),
+        "cet_set_stamps": (c_int, [c_void_p, c_void_p]),
         "cet_timing_read": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
     }
     for name, (res, args) in sig.items():
@@ -68,7 +70,8 @@ EXPORTED = ("cet_last_error", "cet_version", "cet_create_informer", "cet_create_
             "cet_load_weight", "cet_missing_weights", "cet_prob_calls", "cet_set_prob_indices", "cet_seed",
             "cet_native_draw",
             "cet_forward", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
-            "cet_debug_layout", "cet_nmse_split", "cet_timing", "cet_timing_read")
+            "cet_debug_layout", "cet_nmse_split", "cet_timing", "cet_timing_read",
+            "cet_set_variant", "cet_set_stamps")
 
 
 def check(rc: int, what: str = "") -> int:

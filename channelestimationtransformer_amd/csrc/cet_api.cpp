@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -92,6 +93,7 @@ struct cet_engine {
   std::vector<std::string> order;
   bool dirty = true;
   bool uploaded = false;
+  int variant = 2;   // fused-kernel generation (CET_KERNEL=v1 selects the LDS-resident v1)
 
   // packed blobs
   std::vector<uint16_t> wblob;
@@ -121,6 +123,7 @@ struct cet_engine {
   size_t cnt_bytes = 0;
 
   float* dbg = nullptr;
+  unsigned long long* stamps = nullptr;
   std::string dbg_json;
 
   // kernel timing: hipEvents bracketing each forward kernel launch on the caller's stream
@@ -565,6 +568,14 @@ int build_informer(cet_engine* e) {
   p.lds_FLAG = o; o = al(o + NHEAD * 96);
   p.lds_bytes = o;
   p.in_stride = c.enc_in + 4;
+  // v2: bf16 activation image | context/FFN hidden/staged input | stack output | LN partials | scratch
+  o = 0;
+  p.lds2_XB = o; o = al(o + LP * BS * 2);
+  p.lds2_CTX = o; o = al(o + std::max(LP * BS * 2, LP * p.in_stride * 4));
+  p.lds2_ENC = o; o = al(o + SP * BS * 2);
+  p.lds2_LN = o; o = al(o + LP * 8 * 4);
+  p.lds2_SCR = o; o = al(o + 4 * 176 * 4);
+  p.lds2_bytes = o;
   return CET_OK;
 }
 
@@ -803,6 +814,7 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   auto e = std::make_unique<cet_engine>();
   e->kind = 0;
   e->icfg = *cfg;
+  if (const char* v = std::getenv("CET_KERNEL")) e->variant = (std::strcmp(v, "v1") == 0) ? 1 : 2;
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
   const auto& c = *cfg;
@@ -1015,11 +1027,27 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.out = out;
   a.attns = (attns && e->icfg.output_attention) ? attns : nullptr;
   a.dbg = e->dbg;
+  a.stamps = e->stamps;
   a.B = B;
   const int tk = timing_mark(e, st);
-  rc = cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
+  rc = e->variant == 1 ? cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st)
+                       : cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
+  return CET_OK;
+}
+
+int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  e->stamps = reinterpret_cast<unsigned long long*>(stamps_dev);
+  return CET_OK;
+}
+
+int cet_set_variant(cet_engine* e, int variant) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (variant != 1 && variant != 2) return fail(CET_E_INVALID, "variant must be 1 or 2");
+  if (e->kind != 0 && variant != 1) return fail(CET_E_INVALID, "the Transformer engine has one variant");
+  e->variant = variant;
   return CET_OK;
 }
 

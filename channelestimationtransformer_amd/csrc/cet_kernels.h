@@ -7,6 +7,8 @@
 
 namespace cet {
 
+constexpr int MAX_STAMPS = 128;
+
 struct InformerArgs {
   const InformerPlan* plan;   // device copy of the plan
   const void* weights;        // packed bf16 fragment blob
@@ -17,6 +19,7 @@ struct InformerArgs {
   float* out;                 // [B][pred_len][c_out]
   float* attns;               // optional encoder attention maps
   float* dbg;                 // optional per-stage activation dump
+  unsigned long long* stamps; // optional per-phase s_memtime stamps [B][CET_MAX_STAMPS] (diagnostics)
   int B;
 };
 
@@ -34,6 +37,7 @@ struct TransformerArgs {
 }  // namespace cet
 
 extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_informer_v2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_nmse_split(const float* pred, const float* label, int B, int T, int F, float* acc,
                                      float* last, int accumulate, hipStream_t stream);

@@ -77,6 +77,8 @@ struct InformerPlan {
   // LDS layout (byte offsets) and size
   int lds_X, lds_Q, lds_K, lds_VT, lds_ENC, lds_CTX, lds_M, lds_SEL, lds_FLAG, lds_bytes;
   int vts;
+  // v2 (register-resident) kernel LDS layout
+  int lds2_XB, lds2_CTX, lds2_ENC, lds2_LN, lds2_SCR, lds2_bytes;
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
 };

@@ -113,6 +113,14 @@ class Engine:
         check(lib.cet_attns_layout(self._h, offs, lens, n))
         return [(offs[i], lens[i]) for i in range(n)]
 
+    def set_stamps(self, buf) -> None:
+        """Diagnostics: per-phase s_memtime stamps into an int64 device tensor of B·128 (or None)."""
+        check(lib.cet_set_stamps(self._h, ctypes.c_void_p(buf.data_ptr()) if buf is not None else None))
+
+    def set_variant(self, variant: int) -> None:
+        """Fused-kernel generation: 2 (register-resident, default) or 1 (LDS-resident)."""
+        check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
+
     # ------------------------------------------------------------------ kernel timing
     def timing(self, enable: bool) -> None:
         check(lib.cet_timing(self._h, int(enable)), "cet_timing")

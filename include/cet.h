@@ -94,6 +94,13 @@ int cet_attns_layout(cet_engine* e, int64_t* offsets, int* lengths, int max);
 int cet_set_debug(cet_engine* e, float* dbg_dev);
 int64_t cet_debug_floats(cet_engine* e);
 int cet_debug_layout(cet_engine* e, char* json, int buflen);
+/* Diagnostics (v2 kernel): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
+int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
+
+/* Select the fused-kernel generation of an Informer engine: 2 (default, register-resident,
+ * two sequences per CU) or 1 (LDS-resident, one sequence per CU).  CET_KERNEL=v1 in the
+ * environment selects 1 at creation. */
+int cet_set_variant(cet_engine* e, int variant);
 
 /* Kernel timing: when enabled, every cet_forward brackets its kernel launch with a pair of
  * hipEvents on the caller's stream; cet_timing_read() waits for them and returns the summed

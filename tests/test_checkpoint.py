@@ -1,0 +1,45 @@
+"""Reference weight formats round-trip into the engine's model (CPU only)."""
+import numpy as np
+import torch
+
+from channelestimationtransformer_amd.checkpoint import export_json, import_json, load_checkpoint, save_checkpoint
+from channelestimationtransformer_amd.informer import InformerStack
+from golden_util import load_case
+
+
+def _model():
+    return InformerStack(16, 16, 16, 90, 10, 5, 5, 128, 8, [4], 3, 64, 0.05, "prob", "fixed", "gelu", False, True,
+                         torch.device("cpu"))
+
+
+def test_pt_checkpoint_dict_roundtrip(tmp_path):
+    case = load_case("informer_prob_b1")
+    p = str(tmp_path / "tmodel_49.pt")
+    save_checkpoint(p, case.state, epoch=49, global_step=1234)
+    raw = torch.load(p, weights_only=True)
+    assert set(raw) == {"epoch", "model_state_dict", "optimizer_state_dict", "global_step"}
+    state = load_checkpoint(p)
+    m = _model()
+    # the callers load with strict=False (QuantizationAwareTraining.py:200)
+    res = m.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()}, strict=False)
+    assert not res.missing_keys and not res.unexpected_keys
+    for k, v in case.state.items():
+        np.testing.assert_array_equal(m.state_dict()[k].numpy(), v)
+
+
+def test_bare_state_dict_file(tmp_path):
+    case = load_case("transformer_c3")
+    p = str(tmp_path / "sd.pt")
+    torch.save({k: torch.from_numpy(np.asarray(v)) for k, v in case.state.items()}, p)
+    state = load_checkpoint(p)
+    assert set(state) == set(case.state)
+
+
+def test_json_export_roundtrip(tmp_path):
+    case = load_case("informer_prob_b1")
+    d = str(tmp_path / "weight_export")
+    export_json(case.state, d)
+    back = import_json(d)
+    assert set(back) == set(case.state)
+    for k, v in case.state.items():
+        np.testing.assert_array_equal(back[k], v)

@@ -1,0 +1,56 @@
+"""Per-phase cycle breakdown of the v2 fused kernel from in-kernel s_memtime stamps.
+
+Usage (GPU box): python tools/stamps.py [B] > gpurun_out/stamps.txt
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from channelestimationtransformer_amd.dataset import make_batch  # noqa: E402
+
+NAMES = (["start", "embedding"] + sum([[f"L{l} attention", f"L{l} O-proj+LN1", f"L{l} FFN+LN2"] +
+                                       ([f"L{l} conv+pool"] if l < 3 else []) for l in range(4)], []) +
+         ["enc norm", "dec embedding"] +
+         sum([[f"D{l} self-attn", f"D{l} cross-attn", f"D{l} O/LN/FFN rest"] for l in range(3)], []) +
+         ["final norm+proj"])
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    dev = torch.device("cuda:0")
+    m = bench.build_model(dev)
+    eng = m.engine(dev)
+    eng.seed(1)
+    xe, xd, _ = make_batch(B, seed=5)
+    xe = torch.from_numpy(xe).to(dev)
+    xd = torch.from_numpy(xd).to(dev)
+    out = torch.empty(B, 5, 16, device=dev)
+    for _ in range(10):
+        eng.forward(xe, xd, out)
+    st = torch.zeros(B * 128, dtype=torch.int64, device=dev)
+    eng.set_stamps(st)
+    eng.forward(xe, xd, out)
+    torch.cuda.synchronize()
+    eng.set_stamps(None)
+    s = st.view(B, 128).cpu().numpy().astype(np.int64)
+    n = len(NAMES)
+    s = s[:, :n]
+    d = np.diff(s, axis=1)
+    tot = s[:, -1] - s[:, 0]
+    print(f"B={B}  per-WG total cycles: mean {tot.mean():.0f}  min {tot.min()}  max {tot.max()}")
+    start = s[:, 0] - s[:, 0].min()
+    print(f"WG start offsets (cycles): median {np.median(start):.0f}  max {start.max()}  "
+          f"WGs starting after 50% of the kernel: {(start > 0.5 * (s[:, -1].max() - s[:, 0].min())).sum()}")
+    for i in range(1, n):
+        print(f"{NAMES[i]:22s} mean {d[:, i - 1].mean():9.0f}  p10 {np.percentile(d[:, i - 1], 10):9.0f}  "
+              f"p90 {np.percentile(d[:, i - 1], 90):9.0f}  ({100 * d[:, i - 1].mean() / tot.mean():5.1f}%)")
+
+
+if __name__ == "__main__":
+    main()
