@@ -112,6 +112,20 @@ struct cet_engine {
   std::vector<bool> idx_set;
   bool native_rng = false;
   MT19937 rng;
+  // device-resident copy of the same stream (v2 kernel, cet_mt.hpp): two HBM slots of
+  // 624 words + read index; the kernel reads slot mt_cur and writes the advanced state to the
+  // other.  The host mirror lags by host_lag draws and catches up only when it is read.
+  uint32_t* d_mt = nullptr;
+  uint32_t* h_mt = nullptr;
+  hipEvent_t ev_mt = nullptr;
+  bool ev_mt_used = false;
+  int mt_cur = 0;
+  bool dev_mt_valid = false;
+  int64_t host_lag = 0;
+  int64_t draws_per_forward = 0;
+  void sync_host_rng() {
+    for (; host_lag > 0; --host_lag) (void)rng.next();
+  }
 
   // per-forward multiplicity tables (ring of pinned staging + device buffers)
   static constexpr int NSLOT = 4;
@@ -143,6 +157,9 @@ struct cet_engine {
       if (d_cnt[i]) (void)hipFree(d_cnt[i]);
       if (ev[i]) (void)hipEventDestroy(ev[i]);
     }
+    if (d_mt) (void)hipFree(d_mt);
+    if (h_mt) (void)hipHostFree(h_mt);
+    if (ev_mt) (void)hipEventDestroy(ev_mt);
   }
 
   void add(const std::string& name, std::vector<int64_t> shape, bool required = true) {
@@ -363,6 +380,7 @@ int build_informer(cet_engine* e) {
   };
 
   p.C = c.enc_in;
+  p.C_shift = c.enc_in == 8 ? 3 : 4;
   p.c_out = c.c_out;
   p.seq_len = c.seq_len;
   p.dec_len = c.label_len + c.out_len;
@@ -535,7 +553,7 @@ int build_informer(cet_engine* e) {
     ac.LK = e->calls[k].LK;
     ac.U = e->calls[k].U;
     ac.u = u_part(c.factor, ac.LQ);
-    ac.cnt_stride = r16(ac.LK);
+    ac.cnt_stride = 6 * 16;   // fixed 96-byte rows: every key tile of a query row is in bounds
     ac.cnt_off = coff;
     coff += (uint32_t)(r16(ac.LQ) * ac.cnt_stride);
     coff = (coff + 15) & ~15u;
@@ -575,6 +593,11 @@ int build_informer(cet_engine* e) {
   p.lds2_ENC = o; o = al(o + SP * BS * 2);
   p.lds2_LN = o; o = al(o + LP * 8 * 4);
   p.lds2_SCR = o; o = al(o + 4 * 176 * 4);
+  int max_cnt = 0;
+  for (int k = 0; k < p.n_calls; ++k)
+    if (p.calls[k].u < p.calls[k].LQ) max_cnt = std::max(max_cnt, r16(p.calls[k].LQ) * p.calls[k].cnt_stride);
+  p.lds2_CNT = o; o = al(o + max_cnt);
+  p.lds2_MT = o; o = al(o + 624 * 4);
   p.lds2_bytes = o;
   return CET_OK;
 }
@@ -584,8 +607,8 @@ int build_transformer(cet_engine* e);
 int check_informer_config(const cet_informer_config& c) {
   if (c.d_model != DMODEL || c.n_heads != NHEAD)
     return fail(CET_E_INVALID, "this build supports d_model=128, n_heads=8 (head dim 16)");
-  if (c.enc_in != c.dec_in || (c.enc_in % 8) || c.enc_in > 21)
-    return fail(CET_E_INVALID, "enc_in == dec_in, a multiple of 8, <= 21 required");
+  if (c.enc_in != c.dec_in || (c.enc_in != 8 && c.enc_in != 16))
+    return fail(CET_E_INVALID, "enc_in == dec_in in {8, 16} required");
   if (c.d_ff != 64 && c.d_ff != 128) return fail(CET_E_INVALID, "d_ff must be 64 or 128 in this build");
   if (c.seq_len < 2 || c.seq_len > LMAX) return fail(CET_E_INVALID, "seq_len must be in [2, 96]");
   const int Ld = c.label_len + c.out_len;
@@ -639,6 +662,13 @@ int upload(cet_engine* e) {
       if (!e->ev[i]) HIP_TRY(hipEventCreateWithFlags(&e->ev[i], hipEventDisableTiming));
       e->ev_used[i] = false;
     }
+    if (!e->d_mt) {
+      HIP_TRY(hipMalloc((void**)&e->d_mt, 2 * 640 * sizeof(uint32_t)));
+      HIP_TRY(hipHostMalloc((void**)&e->h_mt, 640 * sizeof(uint32_t)));
+      HIP_TRY(hipEventCreateWithFlags(&e->ev_mt, hipEventDisableTiming));
+    }
+    e->draws_per_forward = 0;
+    for (const auto& c : e->calls) e->draws_per_forward += (int64_t)c.LQ * c.U;
   }
   return CET_OK;
 }
@@ -910,6 +940,8 @@ int cet_seed(cet_engine* e, uint64_t seed) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   e->rng.seed(seed);
   e->native_rng = true;
+  e->host_lag = 0;
+  e->dev_mt_valid = false;
   return CET_OK;
 }
 
@@ -920,6 +952,8 @@ int64_t cet_native_draw(cet_engine* e, int32_t* out, int64_t n_max) {
   for (const auto& c : e->calls) n += (int64_t)c.LQ * c.U;
   if (!out) return n;
   if (n_max < n) return fail(CET_E_INVALID, "buffer too small");
+  e->sync_host_rng();
+  e->dev_mt_valid = false;   // the host stream moved past the device copy
   int64_t k = 0;
   for (const auto& c : e->calls)
     for (int i = 0; i < c.LQ * c.U; ++i) out[k++] = (int32_t)(e->rng.next() % (uint32_t)c.LK);
@@ -990,12 +1024,52 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     if (rc) return fail(CET_E_HIP, std::string("transformer launch failed: ") + hipGetErrorString(hipGetLastError()));
     return CET_OK;
   }
-  // ---- this forward's ProbSparse draws → key multiplicity tables
+  const InformerPlan& p = e->ip;
+  InformerArgs a;
+  a.plan = (const InformerPlan*)e->d_plan;
+  a.weights = e->d_w;
+  a.params = e->d_p;
+  a.cnt = nullptr;
+  a.mt_in = nullptr;
+  a.mt_out = nullptr;
+  a.x_enc = x_enc;
+  a.x_dec = x_dec;
+  a.out = out;
+  a.attns = (attns && e->icfg.output_attention) ? attns : nullptr;
+  a.dbg = e->dbg;
+  a.stamps = e->stamps;
+  a.B = B;
+  if (e->variant == 2 && e->native_rng && p.n_calls) {
+    // ---- resident sampler: the kernel replays this forward's draws itself (cet_mt.hpp)
+    if (!e->dev_mt_valid) {
+      e->sync_host_rng();
+      if (e->ev_mt_used) HIP_TRY(hipEventSynchronize(e->ev_mt));
+      std::memcpy(e->h_mt, e->rng.mt, sizeof(e->rng.mt));
+      e->h_mt[624] = (uint32_t)e->rng.idx;
+      HIP_TRY(hipMemcpyAsync(e->d_mt + 640 * e->mt_cur, e->h_mt, 640 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+      HIP_TRY(hipEventRecord(e->ev_mt, st));
+      e->ev_mt_used = true;
+      e->dev_mt_valid = true;
+    }
+    a.mt_in = e->d_mt + 640 * e->mt_cur;
+    a.mt_out = e->d_mt + 640 * (1 - e->mt_cur);
+    e->mt_cur = 1 - e->mt_cur;
+    e->host_lag += e->draws_per_forward;
+    const int tk = timing_mark(e, st);
+    rc = cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
+    if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
+    if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return CET_OK;
+  }
+  // ---- this forward's ProbSparse draws → key multiplicity tables (host-built)
+  if (e->native_rng) {
+    e->sync_host_rng();
+    e->dev_mt_valid = false;
+  }
   const int k = e->slot;
   e->slot = (e->slot + 1) % cet_engine::NSLOT;
   if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
   uint8_t* h = e->h_cnt[k];
-  const InformerPlan& p = e->ip;
   if (p.n_calls) {
     std::memset(h, 0, e->cnt_bytes);
     for (int c = 0; c < p.n_calls; ++c) {
@@ -1017,18 +1091,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     HIP_TRY(hipEventRecord(e->ev[k], st));
     e->ev_used[k] = true;
   }
-  InformerArgs a;
-  a.plan = (const InformerPlan*)e->d_plan;
-  a.weights = e->d_w;
-  a.params = e->d_p;
   a.cnt = e->d_cnt[k];
-  a.x_enc = x_enc;
-  a.x_dec = x_dec;
-  a.out = out;
-  a.attns = (attns && e->icfg.output_attention) ? attns : nullptr;
-  a.dbg = e->dbg;
-  a.stamps = e->stamps;
-  a.B = B;
   const int tk = timing_mark(e, st);
   rc = e->variant == 1 ? cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st)
                        : cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);

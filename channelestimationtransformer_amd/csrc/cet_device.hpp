@@ -45,21 +45,44 @@ __device__ __forceinline__ f32x4 mfma16x16x16(const bf16x4& a, const bf16x4& b, 
                                                    __builtin_bit_cast(short4_t, b), c, 0, 0, 0);
 }
 
-__device__ __forceinline__ bf16x8 cvt8(const f32x4& lo, const f32x4& hi) {
-  bf16x8 r;
-  r[0] = (__bf16)lo[0]; r[1] = (__bf16)lo[1]; r[2] = (__bf16)lo[2]; r[3] = (__bf16)lo[3];
-  r[4] = (__bf16)hi[0]; r[5] = (__bf16)hi[1]; r[6] = (__bf16)hi[2]; r[7] = (__bf16)hi[3];
-  return r;
-}
-__device__ __forceinline__ bf16x4 cvt4(const f32x4& v) {
-  bf16x4 r;
-  r[0] = (__bf16)v[0]; r[1] = (__bf16)v[1]; r[2] = (__bf16)v[2]; r[3] = (__bf16)v[3];
-  return r;
-}
+typedef __attribute__((ext_vector_type(8))) float f32x8;
 
-// XOR-butterfly reductions across the lane axis (full wave or within 16-lane groups).
-__device__ __forceinline__ float xor_sum(float v, int m) { return v + __shfl_xor(v, m, 64); }
-__device__ __forceinline__ float xor_max(float v, int m) { return fmaxf(v, __shfl_xor(v, m, 64)); }
+// fp32 → bf16 (round to nearest even): vector conversions lower to one v_cvt_pk_bf16_f32 per pair
+__device__ __forceinline__ bf16x8 cvt8(const f32x4& lo, const f32x4& hi) {
+  const f32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_convertvector(v, bf16x8);
+}
+__device__ __forceinline__ bf16x4 cvt4(const f32x4& v) { return __builtin_convertvector(v, bf16x4); }
+
+// XOR-butterfly reductions across the lane axis.  The 16- and 32-lane exchanges use gfx950's
+// v_permlane16_swap / v_permlane32_swap (one VALU op, no LDS); with both operands = v the two
+// results are v and its partner, in some order per lane, so their sum/max is the butterfly.
+__device__ __forceinline__ float swap_pair_sum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_pair_sum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_pair_max16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap_pair_max32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor_sum(float v, int m) {
+  if (m == 16) return swap_pair_sum16(v);
+  if (m == 32) return swap_pair_sum32(v);
+  return v + __shfl_xor(v, m, 64);
+}
+__device__ __forceinline__ float xor_max(float v, int m) {
+  if (m == 16) return swap_pair_max16(v);
+  if (m == 32) return swap_pair_max32(v);
+  return fmaxf(v, __shfl_xor(v, m, 64));
+}
 
 // Order LDS traffic of one wave: all earlier LDS ops of this wave complete before later ones
 // are issued, and the compiler may not move memory ops across.  Used where lanes of one wave

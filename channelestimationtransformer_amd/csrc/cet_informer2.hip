@@ -4,20 +4,25 @@
 // Reference: FullPrecision/InformerModel/model.py:142-271, encoder.py:6-106, decoder.py:6-56,
 // attn.py:37-209, embed.py:8-135 (see cet_informer.hip for the v1 kernel and DESIGN.md).
 #include "cet_kernels.h"
+#include "cet_mt.hpp"
 #include "cet_v2.hpp"
 
 namespace cet {
 namespace v2 {
 
 // Token-embedding input for output row m = position m + off (EncoderStack window):
-// A[m][tap·C + c] = x[(m + off - 1 + tap) mod L][c], zero past 3·C.
+// A[m][tap·C + c] = x[(m + off - 1 + tap) mod L][c], zero past 3·C.  C is a power of two
+// (CSH = log2 C) and the wrap is add/subtract — no integer division on the hot path.
 struct LoadEmbedOff {
   const float* X;
-  int L, C, CS, off;
+  int L, CSH, CS, off;
   __device__ __forceinline__ bf16x8 operator()(int m, int k0) const {
-    const int tap = k0 / C, c = k0 - tap * C;
+    const int tap = k0 >> CSH, c = k0 & ((1 << CSH) - 1);
     if (tap >= 3) return bf16x8{};
-    const int r = (m + off - 1 + tap + L) % L;
+    int r = m + off - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded rows (m >= L) only: any valid row
     const f32x4* p = reinterpret_cast<const f32x4*>(X + r * CS + c);
     return cvt8(p[0], p[1]);
   }
@@ -29,7 +34,10 @@ struct LoadCirc3BF16 {
   int L;
   __device__ __forceinline__ bf16x8 operator()(int m, int k0) const {
     const int tap = k0 >> 7, c = k0 & 127;
-    const int r = (m - 1 + tap + L) % L;
+    int r = m - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded rows only
     return *reinterpret_cast<const bf16x8*>(X + r * BS + c);
   }
 };
@@ -61,6 +69,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
   __bf16* CTX = reinterpret_cast<__bf16*>(lds + pl.lds2_CTX);   // attention context / FFN hidden
   __bf16* ENC = reinterpret_cast<__bf16*>(lds + pl.lds2_ENC);
   float* LNP = reinterpret_cast<float*>(lds + pl.lds2_LN);
+  uint8_t* CNT = reinterpret_cast<uint8_t*>(lds + pl.lds2_CNT);
+  MTState gen{reinterpret_cast<uint32_t*>(lds + pl.lds2_MT), MT_N};
   float* SCR = reinterpret_cast<float*>(lds + pl.lds2_SCR) + w * 176;
   float* IN = reinterpret_cast<float*>(lds + pl.lds2_CTX);      // staged raw input (aliases CTX)
   float* dbg = a.dbg ? a.dbg + (size_t)b * pl.dbg_stride : nullptr;
@@ -80,6 +90,10 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       ++sid;
     }
   };
+  if (a.mt_in) {
+    __syncthreads();   // LDS zeroing above is done before the state lands in it
+    mt_load<NTHREADS>(gen, a.mt_in);
+  }   // device-resident sampler (cet_mt.hpp)
   STAMP();
 
   auto attend = [&](const __bf16* Xq, const __bf16* Xkv, const bf16x8* Wq, const bf16x8* Wk, const bf16x8* Wv,
@@ -90,12 +104,29 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     io.dq = dq; io.dk = dk; io.dv = dv;
     io.ctx = CTX; io.LQ = LQ; io.LK = LK; io.prob = prob; io.causal = causal; io.mix = mix; io.u = LQ;
     io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = attn_out; io.m_dbg = nullptr;
+    // sub-phase stamps of the first two sparse calls land in slots 100.. / 108.. (diagnostics)
+    io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
     if (call >= 0) {
       const AttnCall& c = pl.calls[call];
       io.u = c.u;
-      io.cnt = a.cnt + c.cnt_off;
       io.cnt_stride = c.cnt_stride;
       if (dbg && c.m_dbg >= 0) io.m_dbg = dbg + c.m_dbg;
+      const bool sparse = c.u < c.LQ;
+      if (a.mt_in) {
+        // replay this call's draws from the resident mt19937 stream into the LDS table
+        mt_replay<NTHREADS>(gen, c.LQ, c.U, c.LK, sparse ? reinterpret_cast<uint32_t*>(CNT) : nullptr,
+                            c.cnt_stride);
+        if (call == pl.n_calls - 1 && b == 0) mt_store<NTHREADS>(gen, a.mt_out);
+      } else if (sparse) {
+        // stage the host-built table in LDS (one L2 round trip per layer instead of one per
+        // query tile and key tile)
+        const int bytes = ((c.LQ + 15) & ~15) * c.cnt_stride;
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + c.cnt_off);
+        f32x4* dst = reinterpret_cast<f32x4*>(CNT);
+        for (int i = threadIdx.x; i < bytes / 16; i += NTHREADS) dst[i] = src[i];
+        __syncthreads();
+      }
+      if (sparse) io.cnt = CNT;
     }
 #pragma unroll 1
     for (int hh = 0; hh < 2; ++hh) attention_head2(io, P, 2 * w + hh);
@@ -114,10 +145,10 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       for (int mt = 0; mt < MT; ++mt) X.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
       const GemmDesc d = pl.emb_enc;
-      gemm_wave2<2>(W + d.w, nmt, LoadEmbedOff{IN, L0, C, CS, off}, [&](int t, int mt, int n0, f32x4 acc) {
+      gemm_wave2<2>(W, P, d, nmt, LoadEmbedOff{IN, L0, pl.C_shift, CS, off}, [&](int t, int mt, int n0, f32x4 y) {
         const int m = mt * 16 + (lane_id() & 15);
         const int prow = m + off < LMAX ? m + off : LMAX - 1;
-        X.v[t][mt] = affine4(P, d, n0, acc) + load4(P + pl.pe_enc + prow * DMODEL + n0);
+        X.v[t][mt] = y + load4(P + pl.pe_enc + prow * DMODEL + n0);
       });
     }
     __syncthreads();                       // IN (aliases CTX) fully read
@@ -142,8 +173,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       STAMP();  // encoder attention
       {
         const GemmDesc d = ld.o;   // x = x + new_x (encoder.py:49)
-        gemm_wave2<4>(W + d.w, nmt, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 acc) {
-          X.v[t][mt] += affine4(P, d, n0, acc);
+        gemm_wave2<4>(W, P, d, nmt, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
+          X.v[t][mt] += y;
         });
       }
       ln_resid(X, nmt, L, P + ld.ln1.g, P + ld.ln1.b, 1e-5f, false, LNP, Xb);
@@ -152,8 +183,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       {
         const GemmDesc d = ld.f1;  // conv1 (k=1) + activation (encoder.py:52)
         const int relu = pl.act_relu;
-        gemm_tiles<4>(W + d.w, DFF / 16, nmt, LoadBF16{Xb}, [&](int mt, int n0, f32x4 acc) {
-          f32x4 v = affine4(P, d, n0, acc);
+        gemm_tiles<4>(W, P, d, DFF / 16, nmt, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
           *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_id() & 15)) * BS + n0) = cvt4(v);
@@ -162,8 +192,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       __syncthreads();
       {
         const GemmDesc d = ld.f2;  // conv2 (k=1) + residual (encoder.py:53-56)
-        gemm_wave2<DFF / 32>(W + d.w, nmt, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 acc) {
-          X.v[t][mt] += affine4(P, d, n0, acc);
+        gemm_wave2<DFF / 32>(W, P, d, nmt, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
+          X.v[t][mt] += y;
         });
       }
       ln_resid(X, nmt, L, P + ld.ln2.g, P + ld.ln2.b, 1e-5f, false, LNP, Xb);
@@ -178,8 +208,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) Cv.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        gemm_wave2_split<12>(W + d.w, nmt, LoadCirc3BF16{Xb, L}, [&](int t, int mt, int n0, f32x4 acc) {
-          f32x4 v = affine4(P, d, n0, acc);
+        gemm_wave2_split<12>(W, P, d, nmt, LoadCirc3BF16{Xb, L}, [&](int t, int mt, int n0, f32x4 v) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
           Cv.v[t][mt] = v;
@@ -214,10 +243,10 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     for (int mt = 0; mt < MT; ++mt) X.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const GemmDesc d = pl.emb_dec;
-    gemm_wave2<2>(W + d.w, nmd, LoadEmbedOff{IN, Ld, C, CS, 0}, [&](int t, int mt, int n0, f32x4 acc) {
+    gemm_wave2<2>(W, P, d, nmd, LoadEmbedOff{IN, Ld, pl.C_shift, CS, 0}, [&](int t, int mt, int n0, f32x4 y) {
       const int m = mt * 16 + (lane_id() & 15);
       const int prow = m < LMAX ? m : LMAX - 1;
-      X.v[t][mt] = affine4(P, d, n0, acc) + load4(P + pl.pe_dec + prow * DMODEL + n0);
+      X.v[t][mt] = y + load4(P + pl.pe_dec + prow * DMODEL + n0);
     });
   }
   __syncthreads();
@@ -238,8 +267,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     STAMP();  // decoder self-attention
     {
       const GemmDesc d = ld.o;
-      gemm_wave2<4>(W + d.w, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 acc) {
-        X.v[t][mt] += affine4(P, d, n0, acc);
+      gemm_wave2<4>(W, P, d, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
+        X.v[t][mt] += y;
       });
     }
     ln_resid(X, nmd, Ld, P + ld.ln1.g, P + ld.ln1.b, 1e-5f, false, LNP, Xb);
@@ -254,8 +283,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     STAMP();  // cross-attention
     {
       const GemmDesc d = ld.co;
-      gemm_wave2<4>(W + d.w, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 acc) {
-        X.v[t][mt] += affine4(P, d, n0, acc);
+      gemm_wave2<4>(W, P, d, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
+        X.v[t][mt] += y;
       });
     }
     ln_resid(X, nmd, Ld, P + ld.ln2.g, P + ld.ln2.b, 1e-5f, false, LNP, Xb);
@@ -263,8 +292,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     {
       const GemmDesc d = ld.f1;
       const int relu = pl.act_relu;
-      gemm_tiles<4>(W + d.w, DFF / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 acc) {
-        f32x4 v = affine4(P, d, n0, acc);
+      gemm_tiles<4>(W, P, d, DFF / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
         *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_id() & 15)) * BS + n0) = cvt4(v);
@@ -273,8 +301,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     __syncthreads();
     {
       const GemmDesc d = ld.f2;
-      gemm_wave2<DFF / 32>(W + d.w, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 acc) {
-        X.v[t][mt] += affine4(P, d, n0, acc);
+      gemm_wave2<DFF / 32>(W, P, d, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
+        X.v[t][mt] += y;
       });
     }
     ln_resid(X, nmd, Ld, P + ld.ln3.g, P + ld.ln3.b, 1e-5f, false, LNP, Xb);
@@ -290,10 +318,9 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     const GemmDesc d = pl.proj;
     const int first_row = Ld - pl.pred_len, co = pl.c_out;
     float* out = a.out + (size_t)b * pl.pred_len * co;
-    gemm_tiles<4>(W + d.w, d.n / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 acc) {
+    gemm_tiles<4>(W, P, d, d.n / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
       const int m = mt * 16 + (lane_id() & 15);
       if (m < first_row || m >= Ld) return;
-      const f32x4 v = affine4(P, d, n0, acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (n0 + r < co) out[(m - first_row) * co + n0 + r] = v[r];

@@ -13,7 +13,9 @@ struct InformerArgs {
   const InformerPlan* plan;   // device copy of the plan
   const void* weights;        // packed bf16 fragment blob
   const float* params;        // fp32 blob: biases, scales, LN, positional tables
-  const uint8_t* cnt;         // per-forward ProbSparse key multiplicities
+  const uint8_t* cnt;         // per-forward ProbSparse key multiplicities (host-built), or
+  const uint32_t* mt_in;      // v2: resident mt19937 state slot to replay the draws from, and
+  uint32_t* mt_out;           //     the slot workgroup 0 writes the advanced state to
   const float* x_enc;         // [B][seq_len][C]
   const float* x_dec;         // [B][dec_len][C]
   float* out;                 // [B][pred_len][c_out]

@@ -1,0 +1,98 @@
+// Device-resident ProbSparse index sampler: the torch CPU generator's mt19937 stream, regenerated
+// by every workgroup in LDS, so a forward needs no host draw and no host→device copy.
+//
+// The reference draws ``torch.randint(L_K, (L_Q, sample_k))`` once per ProbAttention call
+// (FullPrecision/InformerModel/attn.py:57-60) from the global CPU generator: 32-bit mt19937
+// outputs reduced ``% L_K``, consumed in call order.  The state (624 words + read index) lives in
+// HBM in two ping-pong slots; every workgroup of a forward reads slot ``in``, replays the draws of
+// each call into its LDS key-multiplicity table, and workgroup 0 stores the advanced state into
+// slot ``out`` for the next forward.  The host mirror of the same generator is cet_api.cpp MT19937.
+#pragma once
+#include "cet_device.hpp"
+
+namespace cet {
+
+constexpr int MT_N = 624;
+constexpr int MT_WORDS = 640;   // state + read index, padded (one HBM slot)
+
+struct MTState {
+  uint32_t* st;   // LDS copy of the 624-word state
+  int idx;        // next word to temper (uniform across the workgroup); 624 = twist first
+};
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+// In-place twist in three dependency phases: word i reads i+1 (still old except 623→0) and
+// (i+397) mod 624, which is old for i < 227 and was rewritten by the previous phase otherwise.
+template <int NT>
+__device__ __forceinline__ void mt_twist(uint32_t* st) {
+  static_assert(NT >= 227, "one word per thread per phase");
+  __syncthreads();   // every reader of the previous block is done
+  const int lo[3] = {0, 227, 454}, hi[3] = {227, 454, MT_N};
+#pragma unroll
+  for (int ph = 0; ph < 3; ++ph) {
+    const int i = lo[ph] + (int)threadIdx.x;
+    uint32_t v = 0;
+    if (i < hi[ph]) {
+      const int i1 = i + 1 == MT_N ? 0 : i + 1;
+      const int im = i + 397 >= MT_N ? i + 397 - MT_N : i + 397;
+      const uint32_t y = (st[i] & 0x80000000u) | (st[i1] & 0x7fffffffu);
+      v = st[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    __syncthreads();
+    if (i < hi[ph]) st[i] = v;
+    __syncthreads();
+  }
+}
+
+// Replay one call's L_Q·U draws.  With ``tab`` (LDS, rows of ``stride`` bytes, zeroed here) each
+// draw (q, key) increments tab[q][key]; without it the stream is only advanced (calls whose u ≥ L_Q
+// attend over every query, but the reference still draws their samples).
+template <int NT>
+__device__ __forceinline__ void mt_replay(MTState& g, int LQ, int U, int LK, uint32_t* tab, int stride) {
+  if (tab) {
+    const int words = ((LQ + 15) & ~15) * stride / 4;
+    for (int i = threadIdx.x; i < words; i += NT) tab[i] = 0u;
+    __syncthreads();
+  }
+  const int n = LQ * U;
+  int done = 0;
+  while (done < n) {
+    if (g.idx >= MT_N) {
+      mt_twist<NT>(g.st);
+      g.idx = 0;
+    }
+    const int take = min(MT_N - g.idx, n - done);
+    if (tab) {
+      for (int t = threadIdx.x; t < take; t += NT) {
+        const uint32_t key = mt_temper(g.st[g.idx + t]) % (uint32_t)LK;
+        const int q = (done + t) / U;
+        atomicAdd(&tab[(q * stride + (int)key) >> 2], 1u << ((key & 3u) * 8u));   // counts ≤ U < 256
+      }
+    }
+    done += take;
+    g.idx += take;
+  }
+  __syncthreads();
+}
+
+template <int NT>
+__device__ __forceinline__ void mt_load(MTState& g, const uint32_t* __restrict__ src) {
+  for (int i = threadIdx.x; i < MT_N; i += NT) g.st[i] = src[i];
+  g.idx = (int)src[MT_N];
+  __syncthreads();
+}
+
+template <int NT>
+__device__ __forceinline__ void mt_store(const MTState& g, uint32_t* __restrict__ dst) {
+  for (int i = threadIdx.x; i < MT_N; i += NT) dst[i] = g.st[i];
+  if (threadIdx.x == 0) dst[MT_N] = (uint32_t)g.idx;
+}
+
+}  // namespace cet

@@ -57,6 +57,7 @@ struct AttnCall {
 
 struct InformerPlan {
   int C, c_out, seq_len, dec_len, pred_len;
+  int C_shift;              // log2(C)
   int n_enc;
   int enc_layers[MAX_ENC];
   int enc_first[MAX_ENC];   // index of the encoder's first layer in enc[]
@@ -78,7 +79,7 @@ struct InformerPlan {
   int lds_X, lds_Q, lds_K, lds_VT, lds_ENC, lds_CTX, lds_M, lds_SEL, lds_FLAG, lds_bytes;
   int vts;
   // v2 (register-resident) kernel LDS layout
-  int lds2_XB, lds2_CTX, lds2_ENC, lds2_LN, lds2_SCR, lds2_bytes;
+  int lds2_XB, lds2_CTX, lds2_ENC, lds2_LN, lds2_SCR, lds2_CNT, lds2_MT, lds2_bytes;
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
 };

@@ -48,14 +48,20 @@ __device__ __forceinline__ void load_frags(const bf16x8* __restrict__ W, int nt,
   for (int ks = 0; ks < KS; ++ks) a[ks] = W[((size_t)(nt * KS + ks)) * WAVE + lane];
 }
 
-// Dense layer whose output n-tiles 2w, 2w+1 land in the wave's residual fragments.
-//   epi(t, mt, n0, f32x4 acc) consumes the raw accumulator.
+// Dense layer whose output n-tiles 2w, 2w+1 land in the wave's residual fragments.  The
+// epilogue vectors (LSQ/BN scale, bias) are loaded once, before the m-tile loop, and applied
+// here; epi(t, mt, n0, f32x4 y) receives the finished value.
 template <int KS, class BL, class Epi>
-__device__ __forceinline__ void gemm_wave2(const bf16x8* __restrict__ W, int nmt, BL&& bl, Epi&& epi) {
+__device__ __forceinline__ void gemm_wave2(const bf16x8* __restrict__ W, const float* __restrict__ P, const GemmDesc d,
+                                           int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_id(), w = wave_id();
   bf16x8 a0[KS], a1[KS];
-  load_frags<KS>(W, 2 * w, a0);
-  load_frags<KS>(W, 2 * w + 1, a1);
+  load_frags<KS>(W + d.w, 2 * w, a0);
+  load_frags<KS>(W + d.w, 2 * w + 1, a1);
+  const int n0 = 32 * w + (lane >> 4) * 4, n1 = n0 + 16;
+  f32x4 s0 = {1.f, 1.f, 1.f, 1.f}, s1 = s0, b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (d.scale != NONE) { s0 = load4(P + d.scale + n0); s1 = load4(P + d.scale + n1); }
+  if (d.bias != NONE) { b0 = load4(P + d.bias + n0); b1 = load4(P + d.bias + n1); }
   const int kq = (lane >> 4) * 8, mrow = lane & 15;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -67,28 +73,33 @@ __device__ __forceinline__ void gemm_wave2(const bf16x8* __restrict__ W, int nmt
         c0 = mfma16x16x32(a0[ks], b, c0);
         c1 = mfma16x16x32(a1[ks], b, c1);
       }
-      epi(0, mt, 32 * w + (lane >> 4) * 4, c0);
-      epi(1, mt, 32 * w + 16 + (lane >> 4) * 4, c1);
+      epi(0, mt, n0, c0 * s0 + b0);
+      epi(1, mt, n1, c1 * s1 + b1);
     }
   }
 }
 
 // Same, one of the two n-tiles at a time (halves the fragment registers for deep K).
 template <int KS, class BL, class Epi>
-__device__ __forceinline__ void gemm_wave2_split(const bf16x8* __restrict__ W, int nmt, BL&& bl, Epi&& epi) {
+__device__ __forceinline__ void gemm_wave2_split(const bf16x8* __restrict__ W, const float* __restrict__ P,
+                                                 const GemmDesc d, int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_id(), w = wave_id();
   const int kq = (lane >> 4) * 8, mrow = lane & 15;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     bf16x8 a[KS];
-    load_frags<KS>(W, 2 * w + t, a);
+    load_frags<KS>(W + d.w, 2 * w + t, a);
+    const int n0 = 32 * w + 16 * t + (lane >> 4) * 4;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, bi = {0.f, 0.f, 0.f, 0.f};
+    if (d.scale != NONE) sc = load4(P + d.scale + n0);
+    if (d.bias != NONE) bi = load4(P + d.bias + n0);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       if (mt < nmt) {
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
-        epi(t, mt, 32 * w + 16 * t + (lane >> 4) * 4, c);
+        epi(t, mt, n0, c * sc + bi);
       }
     }
   }
@@ -96,17 +107,22 @@ __device__ __forceinline__ void gemm_wave2_split(const bf16x8* __restrict__ W, i
 
 // Dense layer over an arbitrary set of n-tiles (nt = w, w + NW, ...) — FFN hidden, projection.
 template <int KS, class BL, class Epi>
-__device__ __forceinline__ void gemm_tiles(const bf16x8* __restrict__ W, int n_tiles, int nmt, BL&& bl, Epi&& epi) {
+__device__ __forceinline__ void gemm_tiles(const bf16x8* __restrict__ W, const float* __restrict__ P, const GemmDesc d,
+                                           int n_tiles, int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_id(), w = wave_id();
   const int kq = (lane >> 4) * 8, mrow = lane & 15;
   for (int nt = w; nt < n_tiles; nt += NW) {
     bf16x8 a[KS];
-    load_frags<KS>(W, nt, a);
+    load_frags<KS>(W + d.w, nt, a);
+    const int n0 = nt * 16 + (lane >> 4) * 4;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, bi = {0.f, 0.f, 0.f, 0.f};
+    if (d.scale != NONE) sc = load4(P + d.scale + n0);
+    if (d.bias != NONE) bi = load4(P + d.bias + n0);
     for (int mt = 0; mt < nmt; ++mt) {
       f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
-      epi(mt, nt * 16 + (lane >> 4) * 4, c);
+      epi(mt, n0, c * sc + bi);
     }
   }
 }
@@ -122,6 +138,9 @@ __device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const floa
                                          const float* __restrict__ beta, float eps, bool unbiased_std, float* part,
                                          __bf16* Xb, __bf16* Xb2 = nullptr) {
   const int lane = lane_id(), w = wave_id(), g = lane >> 4, c = lane & 15;
+  const int nb = 32 * w + 4 * g;
+  const f32x4 g0 = load4(gamma + nb), g1 = load4(gamma + nb + 16);   // issued before the barrier
+  const f32x4 b0 = load4(beta + nb), b1 = load4(beta + nb + 16);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     if (mt < nmt) {
@@ -145,9 +164,6 @@ __device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const floa
     }
   }
   __syncthreads();
-  const int nb = 32 * w + 4 * g;
-  const f32x4 g0 = load4(gamma + nb), g1 = load4(gamma + nb + 16);
-  const f32x4 b0 = load4(beta + nb), b1 = load4(beta + nb + 16);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     if (mt < nmt) {
@@ -255,6 +271,7 @@ struct HeadIO {
   float* scr;                 // per-wave scratch: M [96] floats, sel [96] int16, flag [96] bytes
   float* attn_out;            // global [H][LQ][LK] of this sequence or nullptr
   float* m_dbg;               // global [H][LQ] or nullptr
+  unsigned long long* st;     // diagnostics: sub-phase s_memtime stamps of head 0, or nullptr
 };
 
 __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* __restrict__ P, int h) {
@@ -266,6 +283,10 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
   float* Msh = io.scr;
   int16_t* sel = reinterpret_cast<int16_t*>(io.scr + 96);
   uint8_t* flag = reinterpret_cast<uint8_t*>(io.scr + 144);
+  auto SUB = [&](int k) {
+    if (io.st && h == 0 && lane == 0) io.st[k] = __builtin_amdgcn_s_memtime();
+  };
+  SUB(0);
 
   // epilogue vectors: q/k features 16h + 4g + r (C rows), v feature 16h + col (C column)
   const int fq = 16 * h + 4 * g;
@@ -298,6 +319,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
       }
     }
   }
+  SUB(1);
   // pass 2: Q tiles (wq stays live: selected queries are re-projected in phase C)
   bf16x8 wq[4];
   load_frags<4>(io.Wq, h, wq);
@@ -316,8 +338,10 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     }
   }
 
+  SUB(2);
   if (sparse) {
-    // ---- sparsity measurement M (attn.py:95-105) from key multiplicities
+    // ---- sparsity measurement M (attn.py:95-105) from key multiplicities (LDS-staged table)
+    const float invLK = 1.0f / (float)LK;
 #pragma unroll 1
     for (int qt = 0; qt < nqt; ++qt) {
       bf16x4 qf = Qf[0];
@@ -334,9 +358,10 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
             const uint32_t cw = *reinterpret_cast<const uint32_t*>(crow + kt * 16);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const uint32_t cc = (cw >> (8 * r)) & 0xffu;
-              sum = cc ? fmaf((float)cc, s[r], sum) : sum;
-              mx = cc ? fmaxf(mx, s[r]) : mx;
+              // rows past L are stale-but-finite bf16 images in v2, so 0·s is exact zero
+              const float cf = (float)((cw >> (8 * r)) & 0xffu);
+              sum = fmaf(cf, s[r], sum);
+              mx = fmaxf(mx, cf != 0.f ? s[r] : NEG_INF);
             }
           }
         }
@@ -344,7 +369,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
         sum = xor_sum(sum, 32);
         mx = xor_max(mx, 16);
         mx = xor_max(mx, 32);
-        const float M = q < LQ ? mx - sum / (float)LK : NEG_INF;
+        const float M = q < LQ ? mx - sum * invLK : NEG_INF;
         if (g == 0) {
           Msh[q] = M;
           if (io.m_dbg && q < LQ) io.m_dbg[h * LQ + q] = M;
@@ -352,25 +377,52 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
       }
     }
     wave_lds_sync();
-    // ---- top-u by rank; ties toward the lower index (torch leaves the order unspecified)
-    const int n4 = (nqt * 16) >> 2;
-    for (int q = lane; q < LQ; q += WAVE) {
-      const float mq = Msh[q];
-      int rank = 0;
-      for (int k4 = 0; k4 < n4; ++k4) {
-        const f32x4 mk = load4(Msh + 4 * k4);
+    SUB(3);
+    // ---- exact top-u: MSB-first radix select of the u-th largest key over the wave's M values
+    //      (ballots + popcounts, no LDS), then ties at the threshold go to the lower index
+    //      (torch leaves topk's tie order unspecified).
+    uint32_t key[MT];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = 4 * k4 + e;
-          rank += (mk[e] > mq) || (mk[e] == mq && k < q);
+    for (int qt = 0; qt < MT; ++qt) {
+      const float m = qt < nqt ? Msh[qt * 16 + col] : NEG_INF;
+      const uint32_t u = __float_as_uint(m);
+      key[qt] = (qt < nqt && qt * 16 + col < LQ) ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0u;
+    }
+    const int uu = io.u;
+    uint32_t tau = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = tau | (1u << bit);
+      int cnt = 0;
+#pragma unroll
+      for (int qt = 0; qt < MT; ++qt)
+        if (qt < nqt) cnt += __popcll(__ballot(key[qt] >= cand) & 0xFFFFull);
+      if (cnt >= uu) tau = cand;
+    }
+    int gt = 0;
+#pragma unroll
+    for (int qt = 0; qt < MT; ++qt)
+      if (qt < nqt) gt += __popcll(__ballot(key[qt] > tau) & 0xFFFFull);
+    const int need = uu - gt;                           // how many threshold ties are taken
+    const unsigned long long below = (1ull << col) - 1ull;
+    int ties_before = 0, sel_before = 0;
+#pragma unroll
+    for (int qt = 0; qt < MT; ++qt) {
+      if (qt < nqt) {
+        const unsigned long long tie = __ballot(key[qt] == tau) & 0xFFFFull;
+        const bool s = key[qt] > tau || (key[qt] == tau && ties_before + __popcll(tie & below) < need);
+        const unsigned long long sm = __ballot(s) & 0xFFFFull;
+        const int q = qt * 16 + col;
+        if (g == 0 && q < LQ) {
+          flag[q] = s;
+          if (s) sel[sel_before + __popcll(sm & below)] = (int16_t)q;
         }
+        ties_before += __popcll(tie);
+        sel_before += __popcll(sm);
       }
-      const bool s = rank < io.u;
-      flag[q] = s;
-      if (s) sel[rank] = (int16_t)q;
     }
     wave_lds_sync();
   }
+  SUB(4);
 
   // ---- softmax(scale·q·Kᵀ [mask])·V for the selected queries (attn.py:109-138 / 57-65)
   const float scale = 0.25f;
@@ -452,6 +504,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     }
   }
 
+  SUB(5);
   if (sparse) {
     // ---- unselected rows keep the initial context (attn.py:116-125)
     if (!io.causal) {
@@ -511,6 +564,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
         }
     }
   }
+  SUB(6);
 }
 
 }  // namespace v2

@@ -121,6 +121,41 @@ def test_native_sampler_matches_explicit_indices():
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
+def test_resident_sampler_continues_the_stream():
+    """The v2 kernel replays the mt19937 stream on the device (cet_mt.hpp); forwards, host draws
+    and forwards interleaved must consume exactly the draws torch.randint would, in order."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case("informer_prob_b4")
+    m = model_for(case)
+    dev = torch.device("cuda:0")
+    eng = m.engine(dev)
+    xe = torch.from_numpy(case.z["x_enc"]).to(dev)
+    xd = torch.from_numpy(case.z["x_dec"]).to(dev)
+    seed = 4242
+    # host mirror: the draws of forwards #1..#5 in stream order
+    shapes = eng.prob_calls()
+    torch.manual_seed(seed)
+    draws = [[torch.randint(lk, shp).numpy() for lk, shp in shapes] for _ in range(5)]
+    eng.seed(seed)
+    outs = []
+    for i in range(3):                      # #1, #2, #3 on the device stream (twists cross forwards)
+        o = torch.empty(4, 5, 16, device=dev)
+        eng.forward(xe, xd, o)
+        outs.append(o)
+    got = eng.native_draw()                 # #4 drawn by the host (catches up, invalidates the device copy)
+    for g, r in zip(got, draws[3]):
+        np.testing.assert_array_equal(g, r)
+    o5 = torch.empty(4, 5, 16, device=dev)
+    eng.forward(xe, xd, o5)                 # #5: state re-uploaded from the host mirror
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs + [o5]):
+        j = i if i < 3 else 4
+        ref, _, _ = run_engine(m, case.z["x_enc"], case.z["x_dec"], draws[j])
+        np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{j + 1}")
+
+
 def test_batch_sharding_is_bitwise_per_sequence():
     """Every sequence is independent: a batch split in shards gives bitwise-identical rows."""
     _gpu()
@@ -180,17 +215,24 @@ def test_lazy_attns_return_value():
     assert rel_nmse(a0.cpu().numpy()[0], case.z["attn_e0_l0"]) < 1e-3
 
 
-def test_nmse_split_kernel():
+@pytest.mark.parametrize("shape", [(300, 5, 16), (512, 5, 16), (1, 5, 16), (37, 20, 16), (64, 7, 3)])
+def test_nmse_split_kernel(shape):
+    """Row-owner fast path (F % 4 == 0) and the per-step fallback (F = 3), plus the running sum."""
     _gpu()
     from channelestimationtransformer_amd.engine import nmse_split
     from oracle.metrics_np import nmse_split as ref_split
 
-    rng = np.random.default_rng(0)
-    p = rng.standard_normal((300, 5, 16)).astype(np.float32)
-    y = rng.standard_normal((300, 5, 16)).astype(np.float32)
+    rng = np.random.default_rng(sum(shape))
+    p = rng.standard_normal(shape).astype(np.float32)
+    y = rng.standard_normal(shape).astype(np.float32)
     dev = torch.device("cuda:0")
-    got = nmse_split(torch.from_numpy(p).to(dev), torch.from_numpy(y).to(dev)).cpu().numpy()
+    pd, yd = torch.from_numpy(p).to(dev), torch.from_numpy(y).to(dev)
+    got = nmse_split(pd, yd).cpu().numpy()
     np.testing.assert_allclose(got, ref_split(p, y), rtol=1e-6)
+    acc = torch.zeros(shape[1], device=dev)
+    for _ in range(3):
+        nmse_split(pd, yd, acc, accumulate=True)
+    np.testing.assert_allclose(acc.cpu().numpy(), 3 * ref_split(p, y), rtol=1e-5)
 
 
 @pytest.mark.parametrize("variant", [1, 2])

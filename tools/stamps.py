@@ -47,6 +47,14 @@ def main():
     start = s[:, 0] - s[:, 0].min()
     print(f"WG start offsets (cycles): median {np.median(start):.0f}  max {start.max()}  "
           f"WGs starting after 50% of the kernel: {(start > 0.5 * (s[:, -1].max() - s[:, 0].min())).sum()}")
+    sub = st.view(B, 128).cpu().numpy().astype(np.int64)
+    SUBN = ["K/V projection", "Q projection", "phase A (M)", "top-u select", "phase C (softmax·V)", "phase D (rest)"]
+    for c, base in ((0, 100), (1, 108)):
+        ss = sub[:, base:base + 7]
+        if not ss.any():
+            continue
+        dd = np.diff(ss, axis=1)
+        print(f"call {c} head 0 sub-phases: " + "  ".join(f"{SUBN[i]} {dd[:, i].mean():.0f}" for i in range(6)))
     for i in range(1, n):
         print(f"{NAMES[i]:22s} mean {d[:, i - 1].mean():9.0f}  p10 {np.percentile(d[:, i - 1], 10):9.0f}  "
               f"p90 {np.percentile(d[:, i - 1], 90):9.0f}  ({100 * d[:, i - 1].mean() / tot.mean():5.1f}%)")
