@@ -592,7 +592,7 @@ int build_informer(cet_engine* e) {
   p.lds2_CTX = o; o = al(o + std::max(LP * BS * 2, LP * p.in_stride * 4));
   p.lds2_ENC = o; o = al(o + SP * BS * 2);
   p.lds2_LN = o; o = al(o + LP * 8 * 4);
-  p.lds2_SCR = o; o = al(o + 4 * 176 * 4);
+  p.lds2_SCR = o; o = al(o + 4 * V2_SCR_FLOATS * 4);
   int max_cnt = 0;
   for (int k = 0; k < p.n_calls; ++k)
     if (p.calls[k].u < p.calls[k].LQ) max_cnt = std::max(max_cnt, r16(p.calls[k].LQ) * p.calls[k].cnt_stride);
@@ -1070,6 +1070,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   e->slot = (e->slot + 1) % cet_engine::NSLOT;
   if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
   uint8_t* h = e->h_cnt[k];
+  const bool v2 = e->variant == 2;
   if (p.n_calls) {
     std::memset(h, 0, e->cnt_bytes);
     for (int c = 0; c < p.n_calls; ++c) {
@@ -1078,12 +1079,18 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
       uint8_t* tab = h + ac.cnt_off;
       if (e->native_rng) {
         for (int q = 0; q < sh.LQ; ++q)
-          for (int j = 0; j < sh.U; ++j) tab[q * ac.cnt_stride + (int)(e->rng.next() % (uint32_t)sh.LK)]++;
+          for (int j = 0; j < sh.U; ++j) {
+            const int key = (int)(e->rng.next() % (uint32_t)sh.LK);
+            tab[q * ac.cnt_stride + (v2 ? cnt_pos_v2(key) : key)]++;
+          }
       } else {
         if (!e->idx_set[c]) return fail(CET_E_STATE, "ProbSparse indices not set for call " + std::to_string(c));
         const int32_t* id = e->idx[c].data();
         for (int q = 0; q < sh.LQ; ++q)
-          for (int j = 0; j < sh.U; ++j) tab[q * ac.cnt_stride + id[q * sh.U + j]]++;
+          for (int j = 0; j < sh.U; ++j) {
+            const int key = id[q * sh.U + j];
+            tab[q * ac.cnt_stride + (v2 ? cnt_pos_v2(key) : key)]++;
+          }
       }
     }
     if (!e->native_rng) e->idx_set.assign(e->calls.size(), false);

@@ -46,6 +46,7 @@ __device__ __forceinline__ f32x4 mfma16x16x16(const bf16x4& a, const bf16x4& b, 
 }
 
 typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(2))) unsigned long long u64x2;
 
 // fp32 → bf16 (round to nearest even): vector conversions lower to one v_cvt_pk_bf16_f32 per pair
 __device__ __forceinline__ bf16x8 cvt8(const f32x4& lo, const f32x4& hi) {

@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
   float* LNP = reinterpret_cast<float*>(lds + pl.lds2_LN);
   uint8_t* CNT = reinterpret_cast<uint8_t*>(lds + pl.lds2_CNT);
   MTState gen{reinterpret_cast<uint32_t*>(lds + pl.lds2_MT), MT_N};
-  float* SCR = reinterpret_cast<float*>(lds + pl.lds2_SCR) + w * 176;
+  float* SCR = reinterpret_cast<float*>(lds + pl.lds2_SCR) + w * V2_SCR_FLOATS;
   float* IN = reinterpret_cast<float*>(lds + pl.lds2_CTX);      // staged raw input (aliases CTX)
   float* dbg = a.dbg ? a.dbg + (size_t)b * pl.dbg_stride : nullptr;
 

@@ -28,27 +28,39 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-// In-place twist in three dependency phases: word i reads i+1 (still old except 623→0) and
-// (i+397) mod 624, which is old for i < 227 and was rewritten by the previous phase otherwise.
+// Twist with thread t owning words t, t+227 and t+454.  Sequentially, word i reads word i+1 while
+// it is still old (except 623, which reads the new word 0) and word (i+397) mod 624, which is old
+// for i < 227 and otherwise the word 227 places below, rewritten earlier in the same twist: for
+// t+227 that is word t and for t+454 word t+227, both this thread's own results.  So all old
+// words are read first and the update needs no exchange between threads.
+__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t far) {
+  const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+  return far ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
 template <int NT>
 __device__ __forceinline__ void mt_twist(uint32_t* st) {
-  static_assert(NT >= 227, "one word per thread per phase");
+  static_assert(NT >= 227, "one word per thread per third");
+  const int t = threadIdx.x;
   __syncthreads();   // every reader of the previous block is done
-  const int lo[3] = {0, 227, 454}, hi[3] = {227, 454, MT_N};
-#pragma unroll
-  for (int ph = 0; ph < 3; ++ph) {
-    const int i = lo[ph] + (int)threadIdx.x;
-    uint32_t v = 0;
-    if (i < hi[ph]) {
-      const int i1 = i + 1 == MT_N ? 0 : i + 1;
-      const int im = i + 397 >= MT_N ? i + 397 - MT_N : i + 397;
-      const uint32_t y = (st[i] & 0x80000000u) | (st[i1] & 0x7fffffffu);
-      v = st[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  uint32_t n0 = 0, n1 = 0, n2 = 0;
+  if (t < 227) {
+    n0 = mt_mix(st[t], st[t + 1], st[t + 397]);
+    n1 = mt_mix(st[t + 227], st[t + 228], n0);
+    if (t < 169) {
+      n2 = mt_mix(st[t + 454], st[t + 455], n1);
+    } else if (t == 169) {   // word 623 reads the new word 0
+      const uint32_t w0 = mt_mix(st[0], st[1], st[397]);
+      n2 = mt_mix(st[623], w0, n1);
     }
-    __syncthreads();
-    if (i < hi[ph]) st[i] = v;
-    __syncthreads();
   }
+  __syncthreads();
+  if (t < 227) {
+    st[t] = n0;
+    st[t + 227] = n1;
+    if (t < 170) st[t + 454] = n2;
+  }
+  __syncthreads();
 }
 
 // Replay one call's L_Q·U draws.  With ``tab`` (LDS, rows of ``stride`` bytes, zeroed here) each
@@ -62,6 +74,7 @@ __device__ __forceinline__ void mt_replay(MTState& g, int LQ, int U, int LK, uin
     __syncthreads();
   }
   const int n = LQ * U;
+  const float invU = 1.0f / (float)U;
   int done = 0;
   while (done < n) {
     if (g.idx >= MT_N) {
@@ -72,8 +85,8 @@ __device__ __forceinline__ void mt_replay(MTState& g, int LQ, int U, int LK, uin
     if (tab) {
       for (int t = threadIdx.x; t < take; t += NT) {
         const uint32_t key = mt_temper(g.st[g.idx + t]) % (uint32_t)LK;
-        const int q = (done + t) / U;
-        atomicAdd(&tab[(q * stride + (int)key) >> 2], 1u << ((key & 3u) * 8u));   // counts ≤ U < 256
+        const int q = (int)(((float)(done + t) + 0.5f) * invU);   // exact: p < 96·96, U ≤ 96
+        atomicAdd(&tab[(q * stride + cnt_word_off((int)key)) >> 2], 1u << ((key & 3u) * 8u));   // counts ≤ U < 256
       }
     }
     done += take;

@@ -2,6 +2,7 @@
 // A plan is built once per engine on the host (shapes, weight offsets, LDS layout) and
 // copied to device memory; the kernels read it through scalar loads.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace cet {
@@ -15,7 +16,14 @@ constexpr int LMAX = 96;             // longest (padded) sequence a workgroup ke
 constexpr int DMODEL = 128;
 constexpr int NHEAD = 8;
 constexpr int XS = 132;   // fp32 row stride (floats) of X-like LDS buffers (+16 B per row)
-constexpr int BS = 136;   // bf16 row stride (elements) of Q/K/ctx-like LDS buffers (+16 B per row)
+constexpr int BS = 136;
+// v2 key-multiplicity row layout: key 16kt + 4g + r sits at byte 24g + 4kt + r of its 96-byte query
+// row, so the lane holding keys 4g..4g+3 of every key tile reads one contiguous 24-byte run.
+// (v1 rows are key-linear.)
+__host__ __device__ inline int cnt_word_off(int key) { return ((key >> 2) & 3) * 24 + (key >> 4) * 4; }
+__host__ __device__ inline int cnt_pos_v2(int key) { return cnt_word_off(key) + (key & 3); }
+// v2 per-wave attention scratch: 96 u64 selection keys | 96 int16 selected rows | 96 flag bytes
+constexpr int V2_SCR_FLOATS = 264;   // bf16 row stride (elements) of Q/K/ctx-like LDS buffers (+16 B per row)
 
 // One dense layer: packed bf16 weights (fragment order) + fp32 epilogue vectors.
 struct GemmDesc {

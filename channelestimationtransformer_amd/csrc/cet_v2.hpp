@@ -172,7 +172,9 @@ __device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const floa
       const float mean = 0.25f * ((p0[0] + p0[2]) + (p1[0] + p1[2]));
       const float d0 = p0[0] - mean, d1 = p0[2] - mean, d2 = p1[0] - mean, d3 = p1[2] - mean;
       const float M2 = (p0[1] + p0[3]) + (p1[1] + p1[3]) + 32.0f * (d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3);
-      const float inv = unbiased_std ? 1.0f / (sqrtf(M2 * (1.0f / 127.0f)) + eps) : 1.0f / sqrtf(M2 * (1.0f / 128.0f) + eps);
+      // v_rsq_f32 / v_rcp_f32 (1 ulp) instead of the IEEE division expansion
+      const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
+                                     : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
       X.v[0][mt] = (X.v[0][mt] - mean) * inv * g0 + b0;
       X.v[1][mt] = (X.v[1][mt] - mean) * inv * g1 + b1;
       if (m < rows) {
@@ -268,7 +270,7 @@ struct HeadIO {
   int LQ, LK, prob, causal, mix, u;
   const uint8_t* cnt;
   int cnt_stride;
-  float* scr;                 // per-wave scratch: M [96] floats, sel [96] int16, flag [96] bytes
+  float* scr;                 // per-wave scratch: keys [96] u64, sel [96] int16, flag [96] bytes
   float* attn_out;            // global [H][LQ][LK] of this sequence or nullptr
   float* m_dbg;               // global [H][LQ] or nullptr
   unsigned long long* st;     // diagnostics: sub-phase s_memtime stamps of head 0, or nullptr
@@ -280,9 +282,9 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
   const int LQ = io.LQ, LK = io.LK;
   const int nkt = (LK + 15) >> 4, nqt = (LQ + 15) >> 4;
   const bool sparse = io.prob && io.u < LQ;
-  float* Msh = io.scr;
-  int16_t* sel = reinterpret_cast<int16_t*>(io.scr + 96);
-  uint8_t* flag = reinterpret_cast<uint8_t*>(io.scr + 144);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(io.scr);
+  int16_t* sel = reinterpret_cast<int16_t*>(io.scr + 192);
+  uint8_t* flag = reinterpret_cast<uint8_t*>(io.scr + 240);
   auto SUB = [&](int k) {
     if (io.st && h == 0 && lane == 0) io.st[k] = __builtin_amdgcn_s_memtime();
   };
@@ -349,13 +351,16 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
       for (int t = 1; t < MT; ++t) qf = qt == t ? Qf[t] : qf;
       {
         const int q = qt * 16 + col;
-        const uint8_t* crow = io.cnt + (size_t)q * io.cnt_stride + g * 4;
+        // this lane's six count words (keys 16kt + 4g + r, kt = 0..5) are contiguous: cnt_pos()
+        const uint2* crow = reinterpret_cast<const uint2*>(io.cnt + (size_t)q * io.cnt_stride + g * 24);
+        const uint2 c01 = crow[0], c23 = crow[1], c45 = crow[2];
+        const uint32_t cws[MT] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
         float sum = 0.f, mx = NEG_INF;
 #pragma unroll
         for (int kt = 0; kt < MT; ++kt) {
           if (kt < nkt) {
             const f32x4 s = mfma16x16x16(Kf[kt], qf, f32x4{0.f, 0.f, 0.f, 0.f});
-            const uint32_t cw = *reinterpret_cast<const uint32_t*>(crow + kt * 16);
+            const uint32_t cw = cws[kt];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               // rows past L are stale-but-finite bf16 images in v2, so 0·s is exact zero
@@ -369,58 +374,75 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
         sum = xor_sum(sum, 32);
         mx = xor_max(mx, 16);
         mx = xor_max(mx, 32);
-        const float M = q < LQ ? mx - sum * invLK : NEG_INF;
+        const float M = mx - sum * invLK;
+        // selection key: order-preserving image of M above, ~q below — a total order in which
+        // equal M go to the lower index (torch leaves topk's tie order unspecified); 0 = padding
+        const uint32_t mu = __float_as_uint(M);
+        const uint32_t hi = (mu & 0x80000000u) ? ~mu : (mu | 0x80000000u);
+        const uint64_t key = q < LQ ? ((uint64_t)hi << 32) | (uint32_t)(0xffff - q) : 0ull;
         if (g == 0) {
-          Msh[q] = M;
+          keys[q] = key;
           if (io.m_dbg && q < LQ) io.m_dbg[h * LQ + q] = M;
         }
       }
     }
     wave_lds_sync();
     SUB(3);
-    // ---- exact top-u: MSB-first radix select of the u-th largest key over the wave's M values
-    //      (ballots + popcounts, no LDS), then ties at the threshold go to the lower index
-    //      (torch leaves topk's tie order unspecified).
-    uint32_t key[MT];
+    // ---- exact top-u by rank: rank(q) = #{j : key_j > key_q}; q is selected iff rank < u and
+    //      lands in sel[rank].  Lane group g counts over keys [g·J, g·J + J), J = 4·nqt.
+    uint64_t myk[MT];
+    int rank[MT];
 #pragma unroll
     for (int qt = 0; qt < MT; ++qt) {
-      const float m = qt < nqt ? Msh[qt * 16 + col] : NEG_INF;
-      const uint32_t u = __float_as_uint(m);
-      key[qt] = (qt < nqt && qt * 16 + col < LQ) ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0u;
+      myk[qt] = qt < nqt ? keys[qt * 16 + col] : ~0ull;
+      rank[qt] = 0;
+    }
+    const int J = 4 * nqt;
+    const uint64_t* kg = keys + g * J;
+#pragma unroll 2
+    for (int j = 0; j < J; j += 2) {
+      const u64x2 kk = *reinterpret_cast<const u64x2*>(kg + j);
+#pragma unroll
+      for (int qt = 0; qt < MT; ++qt) rank[qt] += (int)(kk[0] > myk[qt]) + (int)(kk[1] > myk[qt]);
     }
     const int uu = io.u;
-    uint32_t tau = 0;
-    for (int bit = 31; bit >= 0; --bit) {
-      const uint32_t cand = tau | (1u << bit);
-      int cnt = 0;
-#pragma unroll
-      for (int qt = 0; qt < MT; ++qt)
-        if (qt < nqt) cnt += __popcll(__ballot(key[qt] >= cand) & 0xFFFFull);
-      if (cnt >= uu) tau = cand;
-    }
-    int gt = 0;
-#pragma unroll
-    for (int qt = 0; qt < MT; ++qt)
-      if (qt < nqt) gt += __popcll(__ballot(key[qt] > tau) & 0xFFFFull);
-    const int need = uu - gt;                           // how many threshold ties are taken
-    const unsigned long long below = (1ull << col) - 1ull;
-    int ties_before = 0, sel_before = 0;
 #pragma unroll
     for (int qt = 0; qt < MT; ++qt) {
       if (qt < nqt) {
-        const unsigned long long tie = __ballot(key[qt] == tau) & 0xFFFFull;
-        const bool s = key[qt] > tau || (key[qt] == tau && ties_before + __popcll(tie & below) < need);
-        const unsigned long long sm = __ballot(s) & 0xFFFFull;
+        int r = rank[qt];
+        r = (int)xor_sum((float)r, 16);     // counts < 2^24: exact in fp32
+        r = (int)xor_sum((float)r, 32);
         const int q = qt * 16 + col;
         if (g == 0 && q < LQ) {
+          const bool s = r < uu;
           flag[q] = s;
-          if (s) sel[sel_before + __popcll(sm & below)] = (int16_t)q;
+          if (s) sel[r] = (int16_t)q;
         }
-        ties_before += __popcll(tie);
-        sel_before += __popcll(sm);
       }
     }
     wave_lds_sync();
+  }
+  if (sparse && !io.causal) {
+    // ---- unselected rows keep the initial context, mean(V) (attn.py:116-119): written to every
+    //      row here, then the selected rows are overwritten below (same wave, LDS in order)
+    float part = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < MT; ++kt)
+      if (kt < nkt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          part += (kt * 16 + g * 4 + j < LK) ? (float)Vf[kt][j] : 0.f;
+    part = xor_sum(part, 16);
+    part = xor_sum(part, 32);
+    const __bf16 mean = (__bf16)(part / (float)LK);
+    if (!io.mix) {
+      for (int q = g; q < LQ; q += 4) io.ctx[q * BS + h * 16 + col] = mean;
+    } else {
+      for (int q = g; q < LQ; q += 4) {
+        const int f = h * LQ * 16 + q * 16 + col;
+        io.ctx[(f >> 7) * BS + (f & 127)] = mean;
+      }
+    }
   }
   SUB(4);
 
@@ -484,7 +506,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     }
     sum = xor_sum(sum, 16);
     sum = xor_sum(sum, 32);
-    const float inv = 1.0f / sum;
+    const float inv = __builtin_amdgcn_rcpf(sum);
     if (i < nsel) {
       store_ctx4(io.ctx, io.mix, LQ, h, qi, g * 4, o * inv);
       if (io.attn_out) {
@@ -506,29 +528,9 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
 
   SUB(5);
   if (sparse) {
-    // ---- unselected rows keep the initial context (attn.py:116-125)
-    if (!io.causal) {
-      float part = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < MT; ++kt)
-        if (kt < nkt)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            part += (kt * 16 + g * 4 + j < LK) ? (float)Vf[kt][j] : 0.f;
-      part = xor_sum(part, 16);
-      part = xor_sum(part, 32);
-      const __bf16 mean = (__bf16)(part / (float)LK);
-      for (int qb = 0; qb < LQ; qb += 4) {
-        const int q = qb + g;
-        if (q < LQ && !flag[q]) {
-          int off;
-          if (!io.mix) off = q * BS + h * 16 + col;
-          else { const int f = h * LQ * 16 + q * 16 + col; off = (f >> 7) * BS + (f & 127); }
-          io.ctx[off] = mean;
-        }
-      }
-    } else {
-      // masked: cumsum(V) = Vᵀ·Tᵀ with T[q][key] = [key <= q] — the same MFMA with an indicator P
+    if (io.causal) {
+      // masked: unselected rows keep cumsum(V) (attn.py:120-125) = Vᵀ·Tᵀ with T[q][key] = [key <= q],
+      // the same MFMA with an indicator P
 #pragma unroll
       for (int qt = 0; qt < MT; ++qt) {
         if (qt < nqt) {
