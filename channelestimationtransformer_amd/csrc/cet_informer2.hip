@@ -94,6 +94,10 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     __syncthreads();   // LDS zeroing above is done before the state lands in it
     mt_load<NTHREADS>(gen, a.mt_in);
   }   // device-resident sampler (cet_mt.hpp)
+  // fine-grained stamps inside encoder layer 0 (slots 116..127, diagnostics)
+  auto FINE = [&](int layer, int k) {
+    if (stamps && layer == 0 && threadIdx.x == 0) stamps[116 + k] = __builtin_amdgcn_s_memtime();
+  };
   STAMP();
 
   auto attend = [&](const __bf16* Xq, const __bf16* Xkv, const bf16x8* Wq, const bf16x8* Wk, const bf16x8* Wv,
@@ -177,6 +181,7 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
           X.v[t][mt] += y;
         });
       }
+      FINE(l, 0);
       ln_resid(X, nmt, L, P + ld.ln1.g, P + ld.ln1.b, 1e-5f, false, LNP, Xb);
       __syncthreads();
       STAMP();  // out-projection + LN1
@@ -189,17 +194,21 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
           *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_id() & 15)) * BS + n0) = cvt4(v);
         });
       }
+      FINE(l, 1);
       __syncthreads();
+      FINE(l, 2);
       {
         const GemmDesc d = ld.f2;  // conv2 (k=1) + residual (encoder.py:53-56)
         gemm_wave2<DFF / 32>(W, P, d, nmt, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
           X.v[t][mt] += y;
         });
       }
+      FINE(l, 3);
       ln_resid(X, nmt, L, P + ld.ln2.g, P + ld.ln2.b, 1e-5f, false, LNP, Xb);
       __syncthreads();
       STAMP();  // FFN + LN2
       if (dbg && ld.dbg_layer >= 0) dump_resid(X, nmt, L, dbg + ld.dbg_layer);
+      FINE(l, 4);
       if (ld.conv.n) {
         // ---- ConvLayer (encoder.py:22-28): circular conv, BN(eval) folded, ELU, MaxPool(3,2,1)
         const GemmDesc d = ld.conv;
@@ -208,15 +217,20 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) Cv.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        gemm_wave2_split<12>(W, P, d, nmt, LoadCirc3BF16{Xb, L}, [&](int t, int mt, int n0, f32x4 v) {
+        with_nmt(nmt, [&](auto NMT) {
+          gemm_wave2_kouter<12, decltype(NMT)::value>(W, P, d, LoadCirc3BF16{Xb, L}, [&](int t, int mt, int n0, f32x4 v) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
-          Cv.v[t][mt] = v;
+            for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
+            Cv.v[t][mt] = v;
+          });
         });
+        FINE(l, 5);
         maxpool_resid(Cv, L, X);
+        FINE(l, 6);
         L = ld.L_out;
         nmt = (L + 15) >> 4;
         __syncthreads();                   // every wave finished reading Xb
+        FINE(l, 7);
         store_xb(X, nmt, L, Xb);
         __syncthreads();
         STAMP();  // distil conv + pool

@@ -105,6 +105,62 @@ __device__ __forceinline__ void gemm_wave2_split(const bf16x8* __restrict__ W, c
   }
 }
 
+// Deep-K dense layer (the distil conv, K = 384) in k-outer order with a compile-time m-tile count:
+// one accumulator per m-tile, and the B fragments of every m-tile for step ks+1 are requested
+// before step ks's MFMAs, so LDS latency overlaps the matrix work instead of preceding each MFMA.
+template <int KS, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_wave2_kouter(const bf16x8* __restrict__ W, const float* __restrict__ P,
+                                                  const GemmDesc d, BL&& bl, Epi&& epi) {
+  const int lane = lane_id(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    bf16x8 a[KS];
+    load_frags<KS>(W + d.w, 2 * w + t, a);
+    const int n0 = 32 * w + 16 * t + (lane >> 4) * 4;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, bi = {0.f, 0.f, 0.f, 0.f};
+    if (d.scale != NONE) sc = load4(P + d.scale + n0);
+    if (d.bias != NONE) bi = load4(P + d.bias + n0);
+    f32x4 c[NMT];
+    bf16x8 b[NMT];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) {
+      c[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      b[mt] = bl(mt * 16 + mrow, kq);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 bn[NMT];
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) bn[mt] = bl(mt * 16 + mrow, (ks + 1) * 32 + kq);
+      }
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) c[mt] = mfma16x16x32(a[ks], b[mt], c[mt]);
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) b[mt] = bn[mt];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance at one k-step
+    }
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) epi(t, mt, n0, c[mt] * sc + bi);
+  }
+}
+
+// Calls f(std::integral_constant<int, n>) for the runtime m-tile count n in [1, MT].
+template <class F>
+__device__ __forceinline__ void with_nmt(int n, F&& f) {
+  switch (n) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    default: f(std::integral_constant<int, 6>{}); break;
+  }
+}
+
 // Dense layer over an arbitrary set of n-tiles (nt = w, w + NW, ...) — FFN hidden, projection.
 template <int KS, class BL, class Epi>
 __device__ __forceinline__ void gemm_tiles(const bf16x8* __restrict__ W, const float* __restrict__ P, const GemmDesc d,

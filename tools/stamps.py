@@ -55,6 +55,14 @@ def main():
             continue
         dd = np.diff(ss, axis=1)
         print(f"call {c} head 0 sub-phases: " + "  ".join(f"{SUBN[i]} {dd[:, i].mean():.0f}" for i in range(6)))
+    # encoder layer 0 fine stamps (slots 116..123) between the phase stamps 2 (attention end) and 5
+    f = sub[:, 116:124]
+    if f.any():
+        pts = np.concatenate([sub[:, 2:3], f[:, 0:1], sub[:, 3:4], f[:, 1:5], f[:, 5:8], sub[:, 5:6]], axis=1)
+        lab = ["O-proj gemm", "LN1", "FFN1+GELU", "barrier", "FFN2 gemm", "LN2", "conv gemm", "maxpool",
+               "barrier", "store_xb+barrier"]
+        dd = np.diff(pts, axis=1).mean(axis=0)
+        print("L0 fine: " + "  ".join(f"{a} {b:.0f}" for a, b in zip(lab, dd)))
     for i in range(1, n):
         print(f"{NAMES[i]:22s} mean {d[:, i - 1].mean():9.0f}  p10 {np.percentile(d[:, i - 1], 10):9.0f}  "
               f"p90 {np.percentile(d[:, i - 1], 90):9.0f}  ({100 * d[:, i - 1].mean() / tot.mean():5.1f}%)")
