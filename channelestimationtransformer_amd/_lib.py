@@ -57,6 +57,11 @@ def _load():
         "cet_set_variant": (c_int, [c_void_p, c_int]),
         "cet_set_stamps": (c_int, [c_void_p, c_void_p]),
         "cet_timing_read": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
+        "cet_prepare_batch": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p,
+                                      c_uint64, c_uint64, c_int, c_int, c_int, c_int, c_double, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p]),
+        "cet_synth_channels": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_double,
+                                       c_void_p, c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -71,7 +76,7 @@ EXPORTED = ("cet_last_error", "cet_version", "cet_create_informer", "cet_create_
             "cet_native_draw",
             "cet_forward", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
             "cet_debug_layout", "cet_nmse_split", "cet_timing", "cet_timing_read",
-            "cet_set_variant", "cet_set_stamps")
+            "cet_set_variant", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
 
 
 def check(rc: int, what: str = "") -> int:

@@ -1151,4 +1151,59 @@ int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, f
   return CET_OK;
 }
 
+int cet_prepare_batch(const float* dataset, int64_t n_samples, int slots, int nr, int nt, const int32_t* sample_idx,
+                      int64_t sample_base, const int32_t* start, const float* noise, uint64_t seed, uint64_t counter,
+                      int B, int seq_len, int label_len, int pred_len, double snr_db, float* x_enc, float* x_dec,
+                      float* label, int32_t* start_out, void* stream) {
+  if (!dataset || !x_enc) return fail(CET_E_INVALID, "null argument");
+  if (B < 0 || n_samples <= 0 || nr <= 0 || nt <= 0 || nr * nt > 64) return fail(CET_E_INVALID, "bad shape");
+  if (seq_len <= 0 || pred_len < 0 || label_len < 0 || label_len > seq_len || slots < seq_len + pred_len)
+    return fail(CET_E_INVALID, "window does not fit: need label_len <= seq_len and seq_len + pred_len <= slots");
+  if (!sample_idx && (sample_base < 0 || sample_base + B > n_samples))
+    return fail(CET_E_INVALID, "sample range outside the dataset");
+  if ((int64_t)slots * nr * nt > (1ll << 30)) return fail(CET_E_INVALID, "sample too large");
+  if (B == 0) return CET_OK;
+  PrepArgs a;
+  a.dataset = reinterpret_cast<const float2*>(dataset);
+  a.n_samples = n_samples;
+  a.slots = slots;
+  a.E = nr * nt;
+  a.sample_idx = sample_idx;
+  a.sample_base = sample_base;
+  a.start = start;
+  a.noise = reinterpret_cast<const float2*>(noise);
+  a.seed = seed;
+  a.counter = counter;
+  a.B = B;
+  a.seq_len = seq_len;
+  a.label_len = label_len;
+  a.pred_len = pred_len;
+  a.noise_scale = (float)std::sqrt(std::pow(10.0, -snr_db / 10.0) / 2.0);   // np.sqrt(sigma / 2) → complex64
+  a.x_enc = x_enc;
+  a.x_dec = x_dec;
+  a.label = label;
+  a.start_out = start_out;
+  if (cet_launch_prepare_batch(&a, (hipStream_t)stream)) return fail(CET_E_HIP, "prepare_batch launch failed");
+  return CET_OK;
+}
+
+int cet_synth_channels(const float* alpha, const float* phi, const float* gain, int n, int slots, int nr, int nt,
+                       int paths, double doppler, float* out, void* stream) {
+  if (!alpha || !phi || !gain || !out) return fail(CET_E_INVALID, "null argument");
+  if (n < 0 || slots <= 0 || nr <= 0 || nt <= 0 || paths <= 0 || nr * nt > 64) return fail(CET_E_INVALID, "bad shape");
+  if (n == 0) return CET_OK;
+  SynthArgs a;
+  a.alpha = alpha;
+  a.phi = phi;
+  a.gain = reinterpret_cast<const float2*>(gain);
+  a.n = n;
+  a.slots = slots;
+  a.E = nr * nt;
+  a.paths = paths;
+  a.doppler = (float)doppler;
+  a.out = reinterpret_cast<float2*>(out);
+  if (cet_launch_synth(&a, (hipStream_t)stream)) return fail(CET_E_HIP, "synth launch failed");
+  return CET_OK;
+}
+
 }  // extern "C"

@@ -25,6 +25,33 @@ struct InformerArgs {
   int B;
 };
 
+// device channel pipeline (cet_data.hip)
+struct PrepArgs {
+  const float2* dataset;   // [n_samples][slots][E] complex64, E = Nr·Nt
+  int64_t n_samples;
+  int slots, E;
+  const int32_t* sample_idx;   // [B] or null: sample = sample_base + b
+  int64_t sample_base;
+  const int32_t* start;        // [B] window starts or null: drawn on device
+  const float2* noise;         // [B][slots][E] (re, im) standard normals, or null: device Philox
+  uint64_t seed, counter;
+  int B, seq_len, label_len, pred_len;
+  float noise_scale;           // sqrt(sigma / 2) rounded to fp32, sigma = 10^(-SNR/10)
+  float* x_enc;                // [B][seq_len][2E]
+  float* x_dec;                // [B][label_len + pred_len][2E] or null
+  float* label;                // [B][pred_len][2E] or null
+  int32_t* start_out;          // [B] the windows used, or null
+};
+
+struct SynthArgs {
+  const float* alpha;
+  const float* phi;
+  const float2* gain;
+  int n, slots, E, paths;
+  float doppler;
+  float2* out;   // [n][slots][E]
+};
+
 struct TransformerArgs {
   const TransformerPlan* plan;
   const void* weights;
@@ -40,6 +67,8 @@ struct TransformerArgs {
 
 extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
+extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_nmse_split(const float* pred, const float* label, int B, int T, int F, float* acc,
                                      float* last, int accumulate, hipStream_t stream);

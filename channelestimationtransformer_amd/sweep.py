@@ -1,0 +1,155 @@
+"""SNR sweep (BASELINE config C4) on the device.
+
+Restates the validation pass ``run_validation`` (FullPrecision/QuantizationAwareTraining.py:86-140)
+at every SNR of ``SNR.sbatch`` (:9-13: 12, 14, 16, 18, 20 dB), with the whole data path on the GPU:
+``DeviceSeqData.batch`` (window, channelnorm, noise, LoadBatch, decoder input) → fused forward →
+``NMSE_Split`` accumulated on the device.  The loader semantics are ``DataLoader(shuffle=True,
+drop_last=True)``: one seeded permutation per SNR, whole batches only, and the reported loss is the
+mean of the per-batch ratios (``loss / len(val_dataloader)``).
+
+Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N -m channelestimationtransformer_amd.sweep``.
+Every rank holds whole reference batches of ``--batch`` sequences; the per-batch ratio sums are
+all-reduced over RCCL at the end of each SNR (no collective in the data path).
+
+Data: ``--dataset`` (a ``.npy`` complex ``[N, slots, 2, 4]``, or a ``.pt`` tensor read with
+``weights_only=True``) or, by default, seeded Jakes channels generated on the device.  Weights:
+``--checkpoint`` (a reference ``.pt``, see checkpoint.py) or the seeded synthetic recipe.
+Prints one JSON line per SNR on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+
+# the reference configuration (FullPrecision/config.py:4-35) and the callers' positional call
+CONFIG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
+              n_heads=8, e_layers=[4], d_layers=3, d_ff=64, dropout=0.05, attn="prob", embed="fixed",
+              activation="gelu", output_attention=False, distil=True)
+
+
+def build_model(device, checkpoint=None, weight_seed=0):
+    import torch
+
+    from .checkpoint import load_checkpoint
+    from .informer import InformerStack
+    from .spec import informer_stack_spec
+    from .weights import synthetic_state_dict
+
+    c = CONFIG
+    m = InformerStack(c["enc_in"], c["dec_in"], c["c_out"], c["seq_len"], c["label_len"], c["pred_len"], c["factor"],
+                      c["d_model"], c["n_heads"], c["e_layers"], c["d_layers"], c["d_ff"], c["dropout"], c["attn"],
+                      c["embed"], c["activation"], c["output_attention"], c["distil"], device)
+    if checkpoint:
+        state = load_checkpoint(checkpoint)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()}, strict=False)
+    else:
+        spec = informer_stack_spec(16, 16, 16, 128, 8, [4], 3, 64, freq="gelu")
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(spec, weight_seed).items()})
+    return m.eval()
+
+
+def load_dataset(path):
+    import torch
+
+    if path.endswith(".npy"):
+        return np.load(path, allow_pickle=False)
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    if not isinstance(obj, torch.Tensor):
+        raise ValueError(f"{path}: expected a complex tensor [N, slots, Nr, Nt]")
+    return obj
+
+
+def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=None, seed=0, rank=0, world=1,
+              device=None, dist=None):
+    """Yields one result dict per SNR (identical on every rank)."""
+    import torch
+
+    from .engine import nmse_split
+    from .pipeline import DeviceSeqData, synth_channels
+
+    c = CONFIG
+    model = build_model(device, checkpoint)
+    eng = model.engine(device)
+    eng.seed(1 + seed)                     # ProbSparse draws: the torch.randint stream, natively
+    if dataset is None:
+        n = n_samples or batch * batches * world
+        dataset = synth_channels(n, slots=100, seed=1234 + seed, device=device)
+    data = DeviceSeqData(dataset, c["seq_len"], c["pred_len"], label_len=c["label_len"], device=device)
+    per_epoch = len(data) // (batch * world)      # drop_last over the global batch
+    n_batches = min(batches, per_epoch) if batches else per_epoch
+    if n_batches == 0:
+        raise ValueError(f"dataset of {len(data)} samples holds no whole batch of {batch} x {world} ranks")
+    F = data.features
+    bufs = (torch.empty(batch, c["seq_len"], F, device=device),
+            torch.empty(batch, c["label_len"] + c["pred_len"], F, device=device),
+            torch.empty(batch, c["pred_len"], F, device=device))
+    out = torch.empty(batch, c["pred_len"], c["c_out"], device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    for k, snr in enumerate(snrs):
+        g = torch.Generator().manual_seed(seed * 1000 + k)
+        perm = torch.randperm(len(data), generator=g).to(torch.int32).to(device)   # the loader's shuffle
+        acc = torch.zeros(c["pred_len"], device=device)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for i in range(n_batches):
+            off = (i * world + rank) * batch
+            xe, xd, lb = data.batch(idx=perm[off:off + batch], seed=seed, counter=(k << 32) + i * world + rank,
+                                    snr=snr, out=bufs, stream=stream)
+            eng.forward(xe, xd, out, None, stream)
+            nmse_split(out, lb, acc, accumulate=True, stream=stream)
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        tot = acc.double()
+        cnt = torch.tensor([float(n_batches)], device=device, dtype=torch.float64)
+        if dist is not None:
+            dist.all_reduce(tot)
+            dist.all_reduce(cnt)
+            t = torch.tensor([dt], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        nmse = (tot / cnt).cpu().numpy()
+        seqs = n_batches * batch * world
+        yield {"snr": snr, "nmse": [float(v) for v in nmse], "nmse_db": [round(float(10 * np.log10(v)), 4) for v in nmse],
+               "nmse_db_mean": round(float(10 * np.log10(nmse.mean())), 4), "batches": int(cnt.item()),
+               "sequences": seqs, "seconds": round(dt, 4), "seq_per_s": round(seqs / dt, 1)}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--snr", type=float, nargs="+", default=[12, 14, 16, 18, 20])
+    ap.add_argument("--batch", type=int, default=512, help="reference batch (sequences per rank per step)")
+    ap.add_argument("--batches", type=int, default=8, help="batches per rank per SNR (0: one epoch)")
+    ap.add_argument("--samples", type=int, default=None, help="synthetic dataset size (default: exactly the batches)")
+    ap.add_argument("--dataset", default=None)
+    ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args(argv)
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    ds = load_dataset(args.dataset) if args.dataset else None
+    for res in run_sweep(args.snr, args.batch, args.batches, ds, args.samples, args.checkpoint, args.seed, rank, world,
+                         dev, dist):
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,11 @@
  *                            FullPrecision/InformerModel/model.py:247-271,
  *                            models/Transformer/model.py:76-87
  *   cet_nmse_split           NMSELossSplit / NMSE_Split_cuda  FullPrecision/metrics.py:26-39
+ *   cet_prepare_batch        SeqData.__getitem__ (window, channelnorm, noise) + LoadBatch + the
+ *                            callers' decoder input: FullPrecision/dataset.py:124-152, :77-88,
+ *                            :54-74, :20-44; QuantizationAwareTraining.py:97-114
+ *   cet_synth_channels       stand-in channel source for the absent CDL dataset pickles
+ *                            (read by SeqData.__init__, FullPrecision/dataset.py:106-115)
  */
 #ifndef CET_H
 #define CET_H
@@ -112,6 +117,30 @@ int cet_timing_read(cet_engine* e, double* total_ms, int64_t* launches);
  * tensors → out_dev[T] (fp32); if accumulate, out_dev[T] += ratio instead of =. */
 int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, float* out_dev, int accumulate,
                    void* stream);
+
+/* Device channel pipeline.  For b < B, sample s = sample_idx ? sample_idx[b] : sample_base + b of
+ * the complex64 dataset [n_samples][slots][nr][nt] (interleaved re, im): normalise to unit mean
+ * power over the whole sample, add complex AWGN of variance 10^(-snr_db/10)·(mean power), window
+ * slots [st, st + seq_len + pred_len) and write, in LoadBatch layout (feature 2·(r·nt + t) + {re, im}):
+ *   x_enc[B][seq_len][2·nr·nt]  the noisy first seq_len slots,
+ *   label[B][pred_len][...]     the clean last pred_len slots (may be NULL),
+ *   x_dec[B][label_len + pred_len][...]  last label_len encoder slots, then zeros (may be NULL).
+ * st = start ? start[b] : a device Philox draw in [0, slots - seq_len - pred_len]; the standard
+ * normals are noise[b][slots][nr][nt][2] when given (parity mode: the reference's two torch.randn
+ * draws) or Philox4x32-10 / Box-Muller draws keyed by (seed, counter, b, element) otherwise.
+ * start_out[B] (may be NULL) receives the windows used.  All arrays are device memory.  A sample
+ * index or window outside the dataset yields NaN rows for that sample. */
+int cet_prepare_batch(const float* dataset, int64_t n_samples, int slots, int nr, int nt, const int32_t* sample_idx,
+                      int64_t sample_base, const int32_t* start, const float* noise, uint64_t seed, uint64_t counter,
+                      int B, int seq_len, int label_len, int pred_len, double snr_db, float* x_enc, float* x_dec,
+                      float* label, int32_t* start_out, void* stream);
+
+/* Seeded sum-of-sinusoids (Jakes) channels, unit mean power per sample:
+ * out[s][t][e] = Σ_p gain[s][e][p]·exp(j(2π·doppler·cos(alpha[s][e][p])·t + phi[s][e][p])) / sqrt(paths),
+ * e = r·nt + a; alpha/phi fp32 [n][nr·nt][paths], gain complex64 [n][nr·nt][paths] (re, im),
+ * out complex64 [n][slots][nr·nt].  Device memory. */
+int cet_synth_channels(const float* alpha, const float* phi, const float* gain, int n, int slots, int nr, int nt,
+                       int paths, double doppler, float* out, void* stream);
 
 #ifdef __cplusplus
 }

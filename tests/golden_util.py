@@ -35,7 +35,7 @@ class Case:
 
 
 def case_names():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz"))
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("data_"))
 
 
 def load_case(name: str) -> Case:

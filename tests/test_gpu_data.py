@@ -1,0 +1,150 @@
+"""Device channel pipeline (cet_prepare_batch / cet_synth_channels) against the data oracle."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+Z = np.load(f"{GOLDEN}/data_seqdata.npz")
+TOL = 2e-6   # fp32 rounding of the two power means, relative to the array's max magnitude
+
+
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _close(got, ref, tol=TOL):
+    got = got.cpu().numpy() if hasattr(got, "cpu") else got
+    np.testing.assert_allclose(got, ref, rtol=0, atol=tol * np.abs(ref).max())
+
+
+def _data(dataset=None, **kw):
+    from channelestimationtransformer_amd.pipeline import DeviceSeqData
+
+    return DeviceSeqData(Z["dataset"] if dataset is None else dataset, int(Z["seq_len"]), int(Z["pred_len"]),
+                         SNR=float(Z["snr"]), label_len=int(Z["label_len"]), device=torch.device("cuda:0"), **kw)
+
+
+def test_prepare_batch_matches_reference_seqdata():
+    """Parity mode: the reference's own draws → the reference's own LoadBatch outputs."""
+    _gpu()
+    d = _data()
+    noise = np.stack([Z["re"], Z["im"]], axis=-1)
+    x_enc, x_dec, label = d.batch(idx=Z["idx"], starts=Z["starts"], noise=noise)
+    torch.cuda.synchronize()
+    _close(x_enc, Z["x_enc"])
+    _close(x_dec, Z["x_dec"])
+    _close(label, Z["label"])
+
+
+def test_reference_rng_protocol_end_to_end():
+    """reference_batch draws from the global generators exactly as __getitem__ would."""
+    _gpu()
+    d = _data()
+    for b, s in enumerate(Z["idx"]):
+        np.random.seed(1000 + b)
+        torch.manual_seed(2000 + b)
+        x_enc, x_dec, label = d.reference_batch([s])
+        _close(x_enc[0], Z["x_enc"][b])
+        _close(label[0], Z["label"][b])
+
+
+def test_device_draws_are_deterministic_in_range_and_normal():
+    _gpu()
+    from oracle.data_np import get_item
+
+    rng = np.random.default_rng(3)
+    n, slots = 64, 100
+    data = (rng.standard_normal((n, slots, 2, 4)) + 1j * rng.standard_normal((n, slots, 2, 4))) * 1.7
+    d = _data(data)
+    a = d.batch(B=n, seed=11, counter=5, return_starts=True)
+    b = d.batch(B=n, seed=11, counter=5, return_starts=True)
+    c = d.batch(B=n, seed=11, counter=6, return_starts=True)
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+    assert not torch.equal(a[0], c[0])
+    st = a[3].cpu().numpy()
+    L = d.length
+    assert st.min() >= 0 and st.max() <= slots - L and len(np.unique(st)) > 1
+    # implied noise = x_enc − clean window: zero mean, variance sigma·(mean power = 1)
+    seq = d.seq_len
+    clean = np.stack([get_item(data[i], int(st[i]), np.zeros((slots, 2, 4)), np.zeros((slots, 2, 4)), d.SNR, seq,
+                               d.pred_len)[2] for i in range(n)])
+    from oracle.data_np import load_batch
+
+    z = a[0].cpu().numpy().astype(np.float64) - load_batch(clean)
+    sigma = 10 ** (-d.SNR / 10)
+    assert abs(z.mean()) < 0.01 * np.sqrt(sigma)
+    assert abs(z.var() / (sigma / 2) - 1.0) < 0.03
+    # labels and decoder inputs stay clean / structured
+    _close(a[2], load_batch(np.stack([get_item(data[i], int(st[i]), np.zeros((slots, 2, 4)), np.zeros((slots, 2, 4)),
+                                               d.SNR, seq, d.pred_len)[3] for i in range(n)])))
+    np.testing.assert_array_equal(a[1][:, d.label_len:].cpu().numpy(), 0.0)
+    assert torch.equal(a[1][:, :d.label_len], a[0][:, seq - d.label_len:])
+
+
+def test_out_of_range_sample_gives_nan_rows_not_a_fault():
+    _gpu()
+    d = _data()
+    x_enc, x_dec, label = d.batch(idx=[0, 99, 2], starts=[0, 0, 1000])
+    torch.cuda.synchronize()
+    assert torch.isfinite(x_enc[0]).all()
+    assert torch.isnan(x_enc[1]).all() and torch.isnan(label[1]).all()
+    assert torch.isnan(x_enc[2]).all() and torch.isnan(x_dec[2]).all()
+
+
+def test_synth_channels_match_oracle():
+    _gpu()
+    from channelestimationtransformer_amd.pipeline import synth_channels
+    from oracle.data_np import jakes
+
+    n, slots, paths, seed, fd = 5, 100, 16, 9, 0.02
+    H = synth_channels(n, slots, seed=seed, doppler=fd, paths=paths, device=torch.device("cuda:0"))
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(seed)
+    alpha = rng.uniform(0, 2 * np.pi, size=(n, 8, paths)).astype(np.float32)
+    phi = rng.uniform(0, 2 * np.pi, size=(n, 8, paths)).astype(np.float32)
+    g = ((rng.standard_normal((n, 8, paths)) + 1j * rng.standard_normal((n, 8, paths))) / np.sqrt(2)).astype(np.complex64)
+    ref = jakes(alpha, phi, g, slots, fd).reshape(n, slots, 2, 4)
+    got = H.cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-5)
+
+
+def test_pipeline_feeds_the_engine():
+    """Device batch → fused forward → NMSE: the same numbers as feeding the host-restated batch."""
+    _gpu()
+    from channelestimationtransformer_amd.engine import nmse_split
+    from engine_util import model_for, run_engine
+    from golden_util import load_case
+    from oracle.data_np import prepare_batch
+
+    case = load_case("informer_prob_b4")
+    m = model_for(case)
+    d = _data()
+    noise = np.stack([Z["re"], Z["im"]], axis=-1)
+    x_enc, x_dec, label = d.batch(idx=Z["idx"], starts=Z["starts"], noise=noise)
+    out_dev, _, _ = run_engine(m, x_enc.cpu().numpy(), x_dec.cpu().numpy(), case.idx)
+    xe, xd, lb = prepare_batch(Z["dataset"], Z["idx"], Z["starts"], Z["re"], Z["im"], float(Z["snr"]),
+                               int(Z["seq_len"]), int(Z["label_len"]), int(Z["pred_len"]))
+    out_host, _, _ = run_engine(m, xe.astype(np.float32), xd.astype(np.float32), case.idx)
+    np.testing.assert_allclose(out_dev, out_host, rtol=0, atol=1e-3 * np.abs(out_host).max())
+    r = nmse_split(torch.from_numpy(out_dev).cuda(), label).cpu().numpy()
+    assert np.all(np.isfinite(r)) and r.shape == (5,)
+
+
+def test_snr_sweep_driver_runs_and_is_deterministic():
+    _gpu()
+    from channelestimationtransformer_amd.sweep import run_sweep
+
+    dev = torch.device("cuda:0")
+    a = list(run_sweep([12, 20], batch=64, batches=2, device=dev))
+    b = list(run_sweep([12, 20], batch=64, batches=2, device=dev))
+    assert [r["snr"] for r in a] == [12, 20]
+    for r, s in zip(a, b):
+        assert r["batches"] == 2 and r["sequences"] == 128 and len(r["nmse_db"]) == 5
+        assert np.all(np.isfinite(r["nmse"]))
+        assert r["nmse"] == s["nmse"]
