@@ -148,3 +148,11 @@ def test_snr_sweep_driver_runs_and_is_deterministic():
         assert r["batches"] == 2 and r["sequences"] == 128 and len(r["nmse_db"]) == 5
         assert np.all(np.isfinite(r["nmse"]))
         assert r["nmse"] == s["nmse"]
+
+
+def test_latency_mode_runs_the_timing_config():
+    _gpu()
+    from channelestimationtransformer_amd.latency import CONFIG, measure
+
+    r = measure(dict(CONFIG), torch.device("cuda:0"), reps=30, warmup=3)
+    assert r["reps"] == 29 and 0 < r["p50_ms"] < 50
