@@ -212,20 +212,23 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       if (ld.conv.n) {
         // ---- ConvLayer (encoder.py:22-28): circular conv, BN(eval) folded, ELU, MaxPool(3,2,1)
         const GemmDesc d = ld.conv;
-        Resid Cv;
+        // Cv lives inside each m-tile-count instantiation and only X leaves it: stores into a
+        // shared Cv would be sunk behind the dispatch through a pointer phi, demoting Cv to scratch
+        with_nmt(nmt, [&](auto NMT) __attribute__((always_inline)) {
+          Resid Cv;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) Cv.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        with_nmt(nmt, [&](auto NMT) {
-          gemm_wave2_kouter<12, decltype(NMT)::value>(W, P, d, LoadCirc3BF16{Xb, L}, [&](int t, int mt, int n0, f32x4 v) {
+            for (int mt = 0; mt < MT; ++mt) Cv.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          gemm_wave2_kouter<12, decltype(NMT)::value>(W, P, d, LoadCirc3BF16{Xb, L},
+                                                      [&](int t, int mt, int n0, f32x4 v) __attribute__((always_inline)) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
             Cv.v[t][mt] = v;
           });
+          FINE(l, 5);
+          maxpool_resid(Cv, L, X);
         });
-        FINE(l, 5);
-        maxpool_resid(Cv, L, X);
         FINE(l, 6);
         L = ld.L_out;
         nmt = (L + 15) >> 4;

@@ -105,47 +105,53 @@ __device__ __forceinline__ void gemm_wave2_split(const bf16x8* __restrict__ W, c
   }
 }
 
+template <int KS, int NMT, int T, class BL, class Epi>
+__device__ __forceinline__ void gemm_kouter_tile(const bf16x8* __restrict__ W, const float* __restrict__ P,
+                                                 const GemmDesc d, BL&& bl, Epi&& epi) {
+  const int lane = lane_id(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  bf16x8 a[KS];
+  load_frags<KS>(W + d.w, 2 * w + T, a);
+  const int n0 = 32 * w + 16 * T + (lane >> 4) * 4;
+  f32x4 sc = {1.f, 1.f, 1.f, 1.f}, bi = {0.f, 0.f, 0.f, 0.f};
+  if (d.scale != NONE) sc = load4(P + d.scale + n0);
+  if (d.bias != NONE) bi = load4(P + d.bias + n0);
+  f32x4 c[NMT];
+  bf16x8 b[NMT];
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    c[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    b[mt] = bl(mt * 16 + mrow, kq);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8 bn[NMT];
+    if (ks + 1 < KS) {
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) bn[mt] = bl(mt * 16 + mrow, (ks + 1) * 32 + kq);
+    }
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) c[mt] = mfma16x16x32(a[ks], b[mt], c[mt]);
+    if (ks + 1 < KS) {
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) b[mt] = bn[mt];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance at one k-step
+  }
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) epi(T, mt, n0, c[mt] * sc + bi);
+}
+
 // Deep-K dense layer (the distil conv, K = 384) in k-outer order with a compile-time m-tile count:
 // one accumulator per m-tile, and the B fragments of every m-tile for step ks+1 are requested
 // before step ks's MFMAs, so LDS latency overlaps the matrix work instead of preceding each MFMA.
+// The n-tile index is a template parameter too, so every residual index the epilogue touches is
+// static (a runtime index would demote the residual to scratch).
 template <int KS, int NMT, class BL, class Epi>
 __device__ __forceinline__ void gemm_wave2_kouter(const bf16x8* __restrict__ W, const float* __restrict__ P,
                                                   const GemmDesc d, BL&& bl, Epi&& epi) {
-  const int lane = lane_id(), w = wave_id();
-  const int kq = (lane >> 4) * 8, mrow = lane & 15;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    bf16x8 a[KS];
-    load_frags<KS>(W + d.w, 2 * w + t, a);
-    const int n0 = 32 * w + 16 * t + (lane >> 4) * 4;
-    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, bi = {0.f, 0.f, 0.f, 0.f};
-    if (d.scale != NONE) sc = load4(P + d.scale + n0);
-    if (d.bias != NONE) bi = load4(P + d.bias + n0);
-    f32x4 c[NMT];
-    bf16x8 b[NMT];
-#pragma unroll
-    for (int mt = 0; mt < NMT; ++mt) {
-      c[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      b[mt] = bl(mt * 16 + mrow, kq);
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 bn[NMT];
-      if (ks + 1 < KS) {
-#pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) bn[mt] = bl(mt * 16 + mrow, (ks + 1) * 32 + kq);
-      }
-#pragma unroll
-      for (int mt = 0; mt < NMT; ++mt) c[mt] = mfma16x16x32(a[ks], b[mt], c[mt]);
-      if (ks + 1 < KS) {
-#pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) b[mt] = bn[mt];
-      }
-      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance at one k-step
-    }
-#pragma unroll
-    for (int mt = 0; mt < NMT; ++mt) epi(t, mt, n0, c[mt] * sc + bi);
-  }
+  gemm_kouter_tile<KS, NMT, 0>(W, P, d, bl, epi);
+  gemm_kouter_tile<KS, NMT, 1>(W, P, d, bl, epi);
 }
 
 // Calls f(std::integral_constant<int, n>) for the runtime m-tile count n in [1, MT].

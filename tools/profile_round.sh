@@ -15,4 +15,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetc
   python "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > /dev/null 2> "$O/pmc_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o pmc -- \
   python "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > /dev/null 2> "$O/pmc_write.err"
+
+cd "$R" && python tools/pmc_traffic.py "$O" --batch 512 -o "$O/pmc_traffic.json" > /dev/null
 echo done > "$O/DONE"
