@@ -10,6 +10,9 @@
 namespace cet {
 namespace v2 {
 
+template <int N>
+using IC = std::integral_constant<int, N>;
+
 // Token-embedding input for output row m = position m + off (EncoderStack window):
 // A[m][tap·C + c] = x[(m + off - 1 + tap) mod L][c], zero past 3·C.  C is a power of two
 // (CSH = log2 C) and the wrap is add/subtract — no integer division on the hot path.
@@ -100,9 +103,11 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
   };
   STAMP();
 
-  auto attend = [&](const __bf16* Xq, const __bf16* Xkv, const bf16x8* Wq, const bf16x8* Wk, const bf16x8* Wv,
-                    GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal, int mix, int call,
-                    float* attn_out) {
+  // MQc / MKc: compile-time bounds on the query / key tiles (std::integral_constant)
+  auto attend = [&](auto MQc, auto MKc, const __bf16* Xq, const __bf16* Xkv, const bf16x8* Wq, const bf16x8* Wk,
+                    const bf16x8* Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
+                    int mix, int call, float* attn_out) {
+    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     HeadIO io;
     io.Xq = Xq; io.Xkv = Xkv; io.Wq = Wq; io.Wk = Wk; io.Wv = Wv;
     io.dq = dq; io.dk = dk; io.dv = dv;
@@ -132,8 +137,14 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       }
       if (sparse) io.cnt = CNT;
     }
+    if constexpr (MQ_ * MK_ >= 4) {
 #pragma unroll 1
-    for (int hh = 0; hh < 2; ++hh) attention_head2(io, P, 2 * w + hh);
+      for (int hh = 0; hh < 2; ++hh) attention_head2<MQ_, MK_>(io, P, 2 * w + hh);
+    } else {
+      // small tiles: both heads in one straight-line block, so their loads and MFMAs overlap
+      attention_head2<MQ_, MK_>(io, P, 2 * w);
+      attention_head2<MQ_, MK_>(io, P, 2 * w + 1);
+    }
   };
 
   for (int e = 0; e < pl.n_enc; ++e) {
@@ -169,8 +180,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
       // ---- AttentionLayer + ProbAttention / FullAttention, two heads per wave, context → CTX
       {
         const GemmDesc q = ld.qkv;
-        attend(Xb, Xb, W + q.w, W + q.w + 8 * FRAGS_PER_TILE4, W + q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
-               part_of(q, 128), part_of(q, 256), L, L, pl.prob, 0, 0, ld.call,
+        attend(IC<MT>{}, IC<MT>{}, Xb, Xb, W + q.w, W + q.w + 8 * FRAGS_PER_TILE4, W + q.w + 16 * FRAGS_PER_TILE4,
+               part_of(q, 0), part_of(q, 128), part_of(q, 256), L, L, pl.prob, 0, 0, ld.call,
                a.attns ? a.attns + ld.attn_off + (size_t)b * ld.attn_stride : nullptr);
       }
       __syncthreads();
@@ -249,101 +260,102 @@ __global__ void __launch_bounds__(NTHREADS, 2) informer_forward_v2(InformerArgs 
     STAMP();  // encoder norm
   }
 
-  // ================================ decoder (decoder.py:43-56)
+  // ================================ decoder (decoder.py:43-56), instantiated for its compile-time
+  // tile count (dec_len ≤ 48): a 1..3-tile residual, branch-free GEMMs, the two heads of a wave
+  // interleaved — the decoder's 15-row layers are latency, not work
   const int Ld = pl.dec_len, S = pl.S;
-  const int nmd = (Ld + 15) >> 4;
   stage(a.x_dec + (size_t)b * Ld * C, IN, Ld, C, CS);
   __syncthreads();
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) X.v[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  {
-    const GemmDesc d = pl.emb_dec;
-    gemm_wave2<2>(W, P, d, nmd, LoadEmbedOff{IN, Ld, pl.C_shift, CS, 0}, [&](int t, int mt, int n0, f32x4 y) {
-      const int m = mt * 16 + (lane_id() & 15);
-      const int prow = m < LMAX ? m : LMAX - 1;
-      X.v[t][mt] = y + load4(P + pl.pe_dec + prow * DMODEL + n0);
-    });
-  }
-  __syncthreads();
-  store_xb(X, nmd, Ld, Xb);
-  __syncthreads();
-  if (dbg) dump_resid(X, nmd, Ld, dbg + pl.dbg_dec_emb);
-  STAMP();  // decoder embedding
+  auto decoder = [&](auto NMDc) __attribute__((always_inline)) {
+    constexpr int NMD = decltype(NMDc)::value;
+    const int nmd = NMD;
+    ResidT<NMD> XD;
+    {
+      const GemmDesc d = pl.emb_dec;
+      gemm_wave2_n<2, NMD>(W, P, d, LoadEmbedOff{IN, Ld, pl.C_shift, CS, 0}, [&](int t, int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_id() & 15);
+        const int prow = m < LMAX ? m : LMAX - 1;
+        XD.v[t][mt] = y + load4(P + pl.pe_dec + prow * DMODEL + n0);
+      });
+    }
+    __syncthreads();
+    store_xb(XD, nmd, Ld, Xb);
+    __syncthreads();
+    if (dbg) dump_resid(XD, nmd, Ld, dbg + pl.dbg_dec_emb);
+    STAMP();  // decoder embedding
 
-  for (int l = 0; l < pl.d_layers; ++l) {
-    const DecLayerDesc& ld = pl.dec[l];
-    {
-      // masked self-attention with the mix scramble (model.py:211-222)
-      const GemmDesc q = ld.qkv;
-      attend(Xb, Xb, W + q.w, W + q.w + 8 * FRAGS_PER_TILE4, W + q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
-             part_of(q, 128), part_of(q, 256), Ld, Ld, pl.prob, 1, pl.mix, ld.call, nullptr);
-    }
-    __syncthreads();
-    STAMP();  // decoder self-attention
-    {
-      const GemmDesc d = ld.o;
-      gemm_wave2<4>(W, P, d, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
-        X.v[t][mt] += y;
-      });
-    }
-    ln_resid(X, nmd, Ld, P + ld.ln1.g, P + ld.ln1.b, 1e-5f, false, LNP, Xb);
-    __syncthreads();
-    {
-      // cross-attention: FullAttention over the encoder-stack output, mix=False
-      const GemmDesc cq = ld.cq, ckv = ld.ckv;
-      attend(Xb, ENC, W + cq.w, W + ckv.w, W + ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0), part_of(ckv, 0),
-             part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
-    }
-    __syncthreads();
-    STAMP();  // cross-attention
-    {
-      const GemmDesc d = ld.co;
-      gemm_wave2<4>(W, P, d, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
-        X.v[t][mt] += y;
-      });
-    }
-    ln_resid(X, nmd, Ld, P + ld.ln2.g, P + ld.ln2.b, 1e-5f, false, LNP, Xb);
-    __syncthreads();
-    {
-      const GemmDesc d = ld.f1;
-      const int relu = pl.act_relu;
-      gemm_tiles<4>(W, P, d, DFF / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+    for (int l = 0; l < pl.d_layers; ++l) {
+      const DecLayerDesc& ld = pl.dec[l];
+      {
+        // masked self-attention with the mix scramble (model.py:211-222)
+        const GemmDesc q = ld.qkv;
+        attend(IC<NMD>{}, IC<NMD>{}, Xb, Xb, W + q.w, W + q.w + 8 * FRAGS_PER_TILE4, W + q.w + 16 * FRAGS_PER_TILE4,
+               part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld, pl.prob, 1, pl.mix, ld.call, nullptr);
+      }
+      __syncthreads();
+      STAMP();  // decoder self-attention
+      {
+        const GemmDesc d = ld.o;
+        gemm_wave2_n<4, NMD>(W, P, d, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) { XD.v[t][mt] += y; });
+      }
+      ln_resid(XD, nmd, Ld, P + ld.ln1.g, P + ld.ln1.b, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      {
+        // cross-attention: FullAttention over the encoder-stack output, mix=False
+        const GemmDesc cq = ld.cq, ckv = ld.ckv;
+        attend(IC<NMD>{}, IC<MT>{}, Xb, ENC, W + cq.w, W + ckv.w, W + ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+               part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
+      }
+      __syncthreads();
+      STAMP();  // cross-attention
+      {
+        const GemmDesc d = ld.co;
+        gemm_wave2_n<4, NMD>(W, P, d, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) { XD.v[t][mt] += y; });
+      }
+      ln_resid(XD, nmd, Ld, P + ld.ln2.g, P + ld.ln2.b, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      {
+        const GemmDesc d = ld.f1;
+        const int relu = pl.act_relu;
+        gemm_tiles_n<4, NMD>(W, P, d, DFF / 16, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
-        *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_id() & 15)) * BS + n0) = cvt4(v);
-      });
+          for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
+          *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_id() & 15)) * BS + n0) = cvt4(v);
+        });
+      }
+      __syncthreads();
+      {
+        const GemmDesc d = ld.f2;
+        gemm_wave2_n<DFF / 32, NMD>(W, P, d, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) { XD.v[t][mt] += y; });
+      }
+      ln_resid(XD, nmd, Ld, P + ld.ln3.g, P + ld.ln3.b, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3
+      if (dbg && ld.dbg >= 0) dump_resid(XD, nmd, Ld, dbg + ld.dbg);
     }
+    ln_resid(XD, nmd, Ld, P + pl.dec_norm.g, P + pl.dec_norm.b, 1e-5f, false, LNP, Xb);
     __syncthreads();
+    if (dbg) dump_resid(XD, nmd, Ld, dbg + pl.dbg_dec_out);
     {
-      const GemmDesc d = ld.f2;
-      gemm_wave2<DFF / 32>(W, P, d, nmd, LoadBF16{CTX}, [&](int t, int mt, int n0, f32x4 y) {
-        X.v[t][mt] += y;
+      // projection (model.py:264) on the last pred_len rows → out[b]
+      const GemmDesc d = pl.proj;
+      const int first_row = Ld - pl.pred_len, co = pl.c_out;
+      float* out = a.out + (size_t)b * pl.pred_len * co;
+      gemm_tiles_n<4, NMD>(W, P, d, d.n / 16, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+        const int m = mt * 16 + (lane_id() & 15);
+        if (m < first_row || m >= Ld) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n0 + r < co) out[(m - first_row) * co + n0 + r] = v[r];
       });
     }
-    ln_resid(X, nmd, Ld, P + ld.ln3.g, P + ld.ln3.b, 1e-5f, false, LNP, Xb);
-    __syncthreads();
-    STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3
-    if (dbg && ld.dbg >= 0) dump_resid(X, nmd, Ld, dbg + ld.dbg);
+    STAMP();  // final norm + projection
+  };
+  switch ((Ld + 15) >> 4) {
+    case 1: decoder(IC<1>{}); break;
+    case 2: decoder(IC<2>{}); break;
+    default: decoder(IC<3>{}); break;
   }
-  ln_resid(X, nmd, Ld, P + pl.dec_norm.g, P + pl.dec_norm.b, 1e-5f, false, LNP, Xb);
-  __syncthreads();
-  if (dbg) dump_resid(X, nmd, Ld, dbg + pl.dbg_dec_out);
-  {
-    // projection (model.py:264) on the last pred_len rows → out[b]
-    const GemmDesc d = pl.proj;
-    const int first_row = Ld - pl.pred_len, co = pl.c_out;
-    float* out = a.out + (size_t)b * pl.pred_len * co;
-    gemm_tiles<4>(W, P, d, d.n / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
-      const int m = mt * 16 + (lane_id() & 15);
-      if (m < first_row || m >= Ld) return;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (n0 + r < co) out[(m - first_row) * co + n0 + r] = v[r];
-    });
-  }
-  STAMP();  // final norm + projection
 }
 
 }  // namespace v2

@@ -24,9 +24,11 @@ constexpr int NW = 4;
 constexpr int NTHREADS = NW * WAVE;
 constexpr int MT = 6;  // max 16-row tiles (96 positions)
 
-struct Resid {
-  f32x4 v[2][MT];
+template <int N>
+struct ResidT {
+  f32x4 v[2][N];
 };
+using Resid = ResidT<MT>;
 
 __device__ __forceinline__ f32x4 load4(const float* __restrict__ p) { return *reinterpret_cast<const f32x4*>(p); }
 
@@ -167,6 +169,67 @@ __device__ __forceinline__ void with_nmt(int n, F&& f) {
   }
 }
 
+// Compile-time m-tile-count forms of gemm_wave2 / gemm_tiles (the decoder runs on 1..3 tiles): no
+// per-tile branches, and the B fragments of tile mt+1 are requested before the MFMAs of tile mt.
+template <int KS, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_wave2_n(const bf16x8* __restrict__ W, const float* __restrict__ P, const GemmDesc d,
+                                             BL&& bl, Epi&& epi) {
+  const int lane = lane_id(), w = wave_id();
+  bf16x8 a0[KS], a1[KS];
+  load_frags<KS>(W + d.w, 2 * w, a0);
+  load_frags<KS>(W + d.w, 2 * w + 1, a1);
+  const int n0 = 32 * w + (lane >> 4) * 4, n1 = n0 + 16;
+  f32x4 s0 = {1.f, 1.f, 1.f, 1.f}, s1 = s0, b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (d.scale != NONE) { s0 = load4(P + d.scale + n0); s1 = load4(P + d.scale + n1); }
+  if (d.bias != NONE) { b0 = load4(P + d.bias + n0); b1 = load4(P + d.bias + n1); }
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  bf16x8 b[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) b[ks] = bl(mrow, ks * 32 + kq);
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    bf16x8 bn[KS];
+    if (mt + 1 < NMT) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bn[ks] = bl((mt + 1) * 16 + mrow, ks * 32 + kq);
+    }
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      c0 = mfma16x16x32(a0[ks], b[ks], c0);
+      c1 = mfma16x16x32(a1[ks], b[ks], c1);
+    }
+    epi(0, mt, n0, c0 * s0 + b0);
+    epi(1, mt, n1, c1 * s1 + b1);
+    if (mt + 1 < NMT) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) b[ks] = bn[ks];
+    }
+  }
+}
+
+template <int KS, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_tiles_n(const bf16x8* __restrict__ W, const float* __restrict__ P,
+                                             const GemmDesc d, int n_tiles, BL&& bl, Epi&& epi) {
+  const int lane = lane_id(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  for (int nt = w; nt < n_tiles; nt += NW) {
+    bf16x8 a[KS];
+    load_frags<KS>(W + d.w, nt, a);
+    const int n0 = nt * 16 + (lane >> 4) * 4;
+    f32x4 sc = {1.f, 1.f, 1.f, 1.f}, bi = {0.f, 0.f, 0.f, 0.f};
+    if (d.scale != NONE) sc = load4(P + d.scale + n0);
+    if (d.bias != NONE) bi = load4(P + d.bias + n0);
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) {
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+      epi(mt, n0, c * sc + bi);
+    }
+  }
+}
+
 // Dense layer over an arbitrary set of n-tiles (nt = w, w + NW, ...) — FFN hidden, projection.
 template <int KS, class BL, class Epi>
 __device__ __forceinline__ void gemm_tiles(const bf16x8* __restrict__ W, const float* __restrict__ P, const GemmDesc d,
@@ -196,7 +259,8 @@ __device__ __forceinline__ void gemm_tiles(const bf16x8* __restrict__ W, const f
 // torch.nn.LayerNorm (biased var, eps in the sqrt) or, if unbiased_std, the reference
 // Transformer's LayerNormalization (alpha·(x-mean)/(std_unbiased+eps)+bias).
 // Contains one workgroup barrier; the caller adds one before Xb is read.
-__device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const float* __restrict__ gamma,
+template <int N>
+__device__ __forceinline__ void ln_resid(ResidT<N>& X, int nmt, int rows, const float* __restrict__ gamma,
                                          const float* __restrict__ beta, float eps, bool unbiased_std, float* part,
                                          __bf16* Xb, __bf16* Xb2 = nullptr) {
   const int lane = lane_id(), w = wave_id(), g = lane >> 4, c = lane & 15;
@@ -204,7 +268,7 @@ __device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const floa
   const f32x4 g0 = load4(gamma + nb), g1 = load4(gamma + nb + 16);   // issued before the barrier
   const f32x4 b0 = load4(beta + nb), b1 = load4(beta + nb + 16);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       float s = 0.f;
 #pragma unroll
@@ -227,7 +291,7 @@ __device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const floa
   }
   __syncthreads();
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       const int m = mt * 16 + c;
       const f32x4 p0 = load4(part + m * 8), p1 = load4(part + m * 8 + 4);
@@ -253,11 +317,12 @@ __device__ __forceinline__ void ln_resid(Resid& X, int nmt, int rows, const floa
 }
 
 // bf16 image of the register residual (rows < rows).
-__device__ __forceinline__ void store_xb(const Resid& X, int nmt, int rows, __bf16* Xb) {
+template <int N>
+__device__ __forceinline__ void store_xb(const ResidT<N>& X, int nmt, int rows, __bf16* Xb) {
   const int lane = lane_id(), w = wave_id();
   const int nb = 32 * w + 4 * (lane >> 4);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       const int m = mt * 16 + (lane & 15);
       if (m < rows) {
@@ -269,11 +334,12 @@ __device__ __forceinline__ void store_xb(const Resid& X, int nmt, int rows, __bf
 }
 
 // fp32 dump of the register residual rows < rows into dst[rows][128] (debug only).
-__device__ __forceinline__ void dump_resid(const Resid& X, int nmt, int rows, float* dst) {
+template <int N>
+__device__ __forceinline__ void dump_resid(const ResidT<N>& X, int nmt, int rows, float* dst) {
   const int lane = lane_id(), w = wave_id();
   const int nb = 32 * w + 4 * (lane >> 4);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       const int m = mt * 16 + (lane & 15);
       if (m < rows) {
@@ -338,6 +404,7 @@ struct HeadIO {
   unsigned long long* st;     // diagnostics: sub-phase s_memtime stamps of head 0, or nullptr
 };
 
+template <int MQ = MT, int MK = MT>
 __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* __restrict__ P, int h) {
   const int lane = lane_id();
   const int col = lane & 15, g = lane >> 4;
@@ -355,7 +422,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
   // epilogue vectors: q/k features 16h + 4g + r (C rows), v feature 16h + col (C column)
   const int fq = 16 * h + 4 * g;
   const int kq = g * 8;
-  bf16x4 Kf[MT], Vf[MT], Qf[MT];
+  bf16x4 Kf[MK], Vf[MK], Qf[MQ];
   {
     // pass 1: K and V tiles from the key/value rows (only wk, wv live)
     bf16x8 wk[4], wv[4];
@@ -367,7 +434,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     const float sv = io.dv.scale != NONE ? P[io.dv.scale + 16 * h + col] : 1.f;
     const float bv = io.dv.bias != NONE ? P[io.dv.bias + 16 * h + col] : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < MK; ++mt) {
       Kf[mt] = bf16x4{};
       Vf[mt] = bf16x4{};
       if (mt < nkt) {
@@ -391,7 +458,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
   if (io.dq.scale != NONE) sq = load4(P + io.dq.scale + fq);
   if (io.dq.bias != NONE) bq = load4(P + io.dq.bias + fq);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+  for (int mt = 0; mt < MQ; ++mt) {
     Qf[mt] = bf16x4{};
     if (mt < nqt) {
       f32x4 q = {0.f, 0.f, 0.f, 0.f};
@@ -410,7 +477,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     for (int qt = 0; qt < nqt; ++qt) {
       bf16x4 qf = Qf[0];
 #pragma unroll
-      for (int t = 1; t < MT; ++t) qf = qt == t ? Qf[t] : qf;
+      for (int t = 1; t < MQ; ++t) qf = qt == t ? Qf[t] : qf;
       {
         const int q = qt * 16 + col;
         // this lane's six count words (keys 16kt + 4g + r, kt = 0..5) are contiguous: cnt_pos()
@@ -419,7 +486,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
         const uint32_t cws[MT] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
         float sum = 0.f, mx = NEG_INF;
 #pragma unroll
-        for (int kt = 0; kt < MT; ++kt) {
+        for (int kt = 0; kt < MK; ++kt) {
           if (kt < nkt) {
             const f32x4 s = mfma16x16x16(Kf[kt], qf, f32x4{0.f, 0.f, 0.f, 0.f});
             const uint32_t cw = cws[kt];
@@ -452,10 +519,10 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     SUB(3);
     // ---- exact top-u by rank: rank(q) = #{j : key_j > key_q}; q is selected iff rank < u and
     //      lands in sel[rank].  Lane group g counts over keys [g·J, g·J + J), J = 4·nqt.
-    uint64_t myk[MT];
-    int rank[MT];
+    uint64_t myk[MQ];
+    int rank[MQ];
 #pragma unroll
-    for (int qt = 0; qt < MT; ++qt) {
+    for (int qt = 0; qt < MQ; ++qt) {
       myk[qt] = qt < nqt ? keys[qt * 16 + col] : ~0ull;
       rank[qt] = 0;
     }
@@ -465,11 +532,11 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     for (int j = 0; j < J; j += 2) {
       const u64x2 kk = *reinterpret_cast<const u64x2*>(kg + j);
 #pragma unroll
-      for (int qt = 0; qt < MT; ++qt) rank[qt] += (int)(kk[0] > myk[qt]) + (int)(kk[1] > myk[qt]);
+      for (int qt = 0; qt < MQ; ++qt) rank[qt] += (int)(kk[0] > myk[qt]) + (int)(kk[1] > myk[qt]);
     }
     const int uu = io.u;
 #pragma unroll
-    for (int qt = 0; qt < MT; ++qt) {
+    for (int qt = 0; qt < MQ; ++qt) {
       if (qt < nqt) {
         int r = rank[qt];
         r = (int)xor_sum((float)r, 16);     // counts < 2^24: exact in fp32
@@ -489,7 +556,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     //      row here, then the selected rows are overwritten below (same wave, LDS in order)
     float part = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < MT; ++kt)
+    for (int kt = 0; kt < MK; ++kt)
       if (kt < nkt)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -531,13 +598,13 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
       qi = ic;
       qs = Qf[0];
 #pragma unroll
-      for (int t = 1; t < MT; ++t) qs = st == t ? Qf[t] : qs;
+      for (int t = 1; t < MQ; ++t) qs = st == t ? Qf[t] : qs;
     }
     // two sweeps over the key tiles (row max, then exp·V): the 16x16x16 score MFMAs are
     // recomputed rather than kept live (registers are the scarce resource at 2 waves/SIMD)
     float mx = NEG_INF;
 #pragma unroll
-    for (int kt = 0; kt < MT; ++kt) {
+    for (int kt = 0; kt < MK; ++kt) {
       if (kt < nkt) {
         const f32x4 a = mfma16x16x16(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
@@ -553,7 +620,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
     float sum = 0.f;
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kt = 0; kt < MT; ++kt) {
+    for (int kt = 0; kt < MK; ++kt) {
       if (kt < nkt) {
         f32x4 p = mfma16x16x16(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
@@ -574,7 +641,7 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
       if (io.attn_out) {
         float* arow = io.attn_out + ((size_t)h * LQ + qi) * LK;
 #pragma unroll
-        for (int kt = 0; kt < MT; ++kt)
+        for (int kt = 0; kt < MK; ++kt)
           if (kt < nkt) {
             const f32x4 p = mfma16x16x16(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
@@ -594,12 +661,12 @@ __device__ __forceinline__ void attention_head2(const HeadIO& io, const float* _
       // masked: unselected rows keep cumsum(V) (attn.py:120-125) = Vᵀ·Tᵀ with T[q][key] = [key <= q],
       // the same MFMA with an indicator P
 #pragma unroll
-      for (int qt = 0; qt < MT; ++qt) {
+      for (int qt = 0; qt < MQ; ++qt) {
         if (qt < nqt) {
           const int q = qt * 16 + col;
           f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int kt = 0; kt < MT; ++kt) {
+          for (int kt = 0; kt < MK; ++kt) {
             if (kt < nkt) {
               f32x4 ind;
 #pragma unroll
