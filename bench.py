@@ -26,6 +26,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
+KERNEL_NAMES = {1: "cet::informer_forward<64>", 2: "cet::v2::informer_forward_v2<64>",
+                3: "cet::v3::informer_forward_v3<64>"}
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
            n_heads=8, e_layers=[4], d_layers=3, d_ff=64, dropout=0.05, attn="prob", embed="fixed",
@@ -95,7 +97,8 @@ def main():
     ap.add_argument("--snr", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--variant", type=int, default=2, help="fused-kernel generation (1: LDS-resident, 2: register-resident)")
+    ap.add_argument("--variant", type=int, default=3,
+                    help="fused-kernel generation (1: LDS-resident, 2: 4-wave register-resident, 3: 8-wave)")
     args = ap.parse_args()
 
     import torch
@@ -208,7 +211,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                          "traffic": load_traffic(os.path.join(ROOT, "profiles")),
-                         "kernel": "cet::v2::informer_forward_v2<64>" if args.variant == 2 else "cet::informer_forward<64>", "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel": KERNEL_NAMES[args.variant], "kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }

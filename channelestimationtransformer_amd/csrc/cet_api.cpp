@@ -93,7 +93,7 @@ struct cet_engine {
   std::vector<std::string> order;
   bool dirty = true;
   bool uploaded = false;
-  int variant = 2;   // fused-kernel generation (CET_KERNEL=v1 selects the LDS-resident v1)
+  int variant = 3;   // fused-kernel generation (CET_KERNEL=v1 / v2 select the older kernels)
 
   // packed blobs
   std::vector<uint16_t> wblob;
@@ -599,6 +599,16 @@ int build_informer(cet_engine* e) {
   p.lds2_CNT = o; o = al(o + max_cnt);
   p.lds2_MT = o; o = al(o + 624 * 4);
   p.lds2_bytes = o;
+  // v3: bf16 image | context/FFN hidden/staged input | stack output | 8 waves' attention scratch,
+  // aliased by the LayerNorm partials | multiplicity table | sampler state (≤ 80 KB: 2 per CU)
+  o = 0;
+  p.lds3_XB = o; o = al(o + LP * BS * 2);
+  p.lds3_CTX = o; o = al(o + std::max(LP * BS * 2, LP * p.in_stride * 4));
+  p.lds3_ENC = o; o = al(o + SP * BS * 2);
+  p.lds3_SCR = o; o = al(o + std::max(LP * LN3_STRIDE * 4, 8 * V2_SCR_FLOATS * 4));
+  p.lds3_CNT = o; o = al(o + max_cnt);
+  p.lds3_MT = o; o = al(o + 624 * 4);
+  p.lds3_bytes = o;
   return CET_OK;
 }
 
@@ -844,7 +854,8 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   auto e = std::make_unique<cet_engine>();
   e->kind = 0;
   e->icfg = *cfg;
-  if (const char* v = std::getenv("CET_KERNEL")) e->variant = (std::strcmp(v, "v1") == 0) ? 1 : 2;
+  if (const char* v = std::getenv("CET_KERNEL"))
+    e->variant = std::strcmp(v, "v1") == 0 ? 1 : (std::strcmp(v, "v2") == 0 ? 2 : 3);
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
   const auto& c = *cfg;
@@ -1000,6 +1011,15 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen) {
   return (int)e->dbg_json.size();
 }
 
+static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
+  const InformerPlan& p = e->ip;
+  switch (e->variant) {
+    case 1: return cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
+    case 2: return cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
+    default: return cet_launch_informer_v3(&a, e->icfg.d_ff, p.lds3_bytes, st);
+  }
+}
+
 int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
                 void* stream) {
   if (!e || !x_enc || !x_dec || !out) return fail(CET_E_INVALID, "null argument");
@@ -1039,7 +1059,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.dbg = e->dbg;
   a.stamps = e->stamps;
   a.B = B;
-  if (e->variant == 2 && e->native_rng && p.n_calls) {
+  if (e->variant >= 2 && e->native_rng && p.n_calls) {
     // ---- resident sampler: the kernel replays this forward's draws itself (cet_mt.hpp)
     if (!e->dev_mt_valid) {
       e->sync_host_rng();
@@ -1056,7 +1076,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     e->mt_cur = 1 - e->mt_cur;
     e->host_lag += e->draws_per_forward;
     const int tk = timing_mark(e, st);
-    rc = cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
+    rc = launch_fused(e, a, st);
     if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
     if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
     return CET_OK;
@@ -1070,7 +1090,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   e->slot = (e->slot + 1) % cet_engine::NSLOT;
   if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
   uint8_t* h = e->h_cnt[k];
-  const bool v2 = e->variant == 2;
+  const bool v2 = e->variant >= 2;   // v2 and v3 share the count-row layout
   if (p.n_calls) {
     std::memset(h, 0, e->cnt_bytes);
     for (int c = 0; c < p.n_calls; ++c) {
@@ -1100,8 +1120,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   }
   a.cnt = e->d_cnt[k];
   const int tk = timing_mark(e, st);
-  rc = e->variant == 1 ? cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st)
-                       : cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
+  rc = launch_fused(e, a, st);
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
   return CET_OK;
@@ -1115,7 +1134,7 @@ int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev) {
 
 int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
-  if (variant != 1 && variant != 2) return fail(CET_E_INVALID, "variant must be 1 or 2");
+  if (variant < 1 || variant > 3) return fail(CET_E_INVALID, "variant must be 1, 2 or 3");
   if (e->kind != 0 && variant != 1) return fail(CET_E_INVALID, "the Transformer engine has one variant");
   e->variant = variant;
   return CET_OK;

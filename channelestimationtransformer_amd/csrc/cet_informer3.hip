@@ -1,0 +1,377 @@
+// Fused InformerStack forward, v3: 512-thread workgroups (8 waves), one residual n-tile and one
+// attention head per wave (cet_v3.hpp), ≤80 KB of LDS and ≤128 VGPRs so two sequences share a CU
+// at 4 waves per SIMD.
+//
+// Reference: FullPrecision/InformerModel/model.py:142-271, encoder.py:6-106, decoder.py:6-56,
+// attn.py:37-209, embed.py:8-135 (the v2 kernel, cet_informer2.hip, has the same phase order).
+#include "cet_kernels.h"
+#include "cet_mt.hpp"
+#include "cet_v3.hpp"
+
+namespace cet {
+namespace v3 {
+
+template <int N>
+using IC = std::integral_constant<int, N>;
+
+// Token-embedding input for output row m = position m + off (EncoderStack window):
+// A[m][tap·C + c] = x[(m + off - 1 + tap) mod L][c], zero past 3·C (C a power of two).
+struct LoadEmbedOff {
+  const float* X;
+  int L, CSH, CS, off;
+  __device__ __forceinline__ bf16x8 operator()(int m, int k0) const {
+    const int tap = k0 >> CSH, c = k0 & ((1 << CSH) - 1);
+    if (tap >= 3) return bf16x8{};
+    int r = m + off - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded rows (m >= L) only: any valid row
+    const f32x4* p = reinterpret_cast<const f32x4*>(X + r * CS + c);
+    return cvt8(p[0], p[1]);
+  }
+};
+
+// Circular k=3 conv input from the bf16 image: A[m][tap·128 + c] = Xb[(m-1+tap) mod L][c].
+struct LoadCirc3BF16 {
+  const __bf16* X;
+  int L;
+  __device__ __forceinline__ bf16x8 operator()(int m, int k0) const {
+    const int tap = k0 >> 7, c = k0 & 127;
+    int r = m - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded rows only
+    return *reinterpret_cast<const bf16x8*>(X + r * BS + c);
+  }
+};
+
+__device__ __forceinline__ void stage(const float* __restrict__ src, float* dst, int L, int C, int CS) {
+  for (int i = threadIdx.x; i < L * C; i += NTHREADS) {
+    const int t = i / C, c = i - t * C;
+    dst[t * CS + c] = src[i];
+  }
+}
+
+// Plan access point.  An opaque (asm) pointer here forces per-phase scalar re-loads and cut SGPR
+// spills, but raised VGPR spills more (measured with -Rpass-analysis), so it stays transparent.
+template <class T>
+__device__ __forceinline__ const T* fresh(const T* p) {
+  return p;
+}
+
+__device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
+  if (d.bias != NONE) d.bias += off;
+  if (d.scale != NONE) d.scale += off;
+  return d;
+}
+
+template <int DFF>
+__global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+#define PL (*fresh(a.plan))
+#define ELD (PL.enc[first + l])
+#define DLD (PL.dec[l])
+  const Mem M{make_rsrc(a.weights), make_rsrc(a.params)};
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  const int w = wave_id();
+
+  __bf16* Xb = reinterpret_cast<__bf16*>(lds + PL.lds3_XB);
+  __bf16* CTX = reinterpret_cast<__bf16*>(lds + PL.lds3_CTX);   // attention context / FFN hidden
+  __bf16* ENC = reinterpret_cast<__bf16*>(lds + PL.lds3_ENC);
+  float* LNP = reinterpret_cast<float*>(lds + PL.lds3_SCR);      // LN partials (alias the scratch)
+  uint8_t* CNT = reinterpret_cast<uint8_t*>(lds + PL.lds3_CNT);
+  MTState gen{reinterpret_cast<uint32_t*>(lds + PL.lds3_MT), MT_N};
+  float* SCR = reinterpret_cast<float*>(lds + PL.lds3_SCR) + w * V2_SCR_FLOATS;
+  float* IN = reinterpret_cast<float*>(lds + PL.lds3_CTX);      // staged raw input (aliases CTX)
+  float* dbg = a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
+
+  // zero the activation images: rows past L of Xb / CTX / ENC are read (never used) by MFMAs
+  for (int i = threadIdx.x; i < PL.lds3_CNT / 16; i += NTHREADS)
+    reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride;
+  constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // bf16x8 per n-tile at K = 128
+  Res<MT> X;
+  // diagnostics: s_memtime at phase boundaries (wave 0, lane 0), off unless a.stamps is set
+  unsigned long long* stamps = a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
+  int sid = 0;
+  auto STAMP = [&]() {
+    if (stamps) {
+      if (threadIdx.x == 0 && sid < MAX_STAMPS) stamps[sid] = __builtin_amdgcn_s_memtime();
+      ++sid;
+    }
+  };
+  if (a.mt_in) {
+    __syncthreads();   // LDS zeroing above is done before the state lands in it
+    mt_load<NTHREADS>(gen, a.mt_in);
+  }   // device-resident sampler (cet_mt.hpp)
+  auto FINE = [&](int layer, int k) {
+    if (stamps && layer == 0 && threadIdx.x == 0) stamps[116 + k] = __builtin_amdgcn_s_memtime();
+  };
+  STAMP();
+
+  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles
+  auto attend = [&](auto MQc, auto MKc, const __bf16* Xq, const __bf16* Xkv, uint32_t Wq, uint32_t Wk,
+                    uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
+                    int mix, int call, float* attn_out) {
+    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    HeadIO io;
+    io.Xq = Xq; io.Xkv = Xkv; io.wq = Wq; io.wk = Wk; io.wv = Wv;
+    io.dq = dq; io.dk = dk; io.dv = dv;
+    io.ctx = CTX; io.LQ = LQ; io.LK = LK; io.prob = prob; io.causal = causal; io.mix = mix; io.u = LQ;
+    io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = attn_out; io.m_dbg = nullptr;
+    io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
+    if (call >= 0) {
+      const AttnCall& c = PL.calls[call];
+      io.u = c.u;
+      io.cnt_stride = c.cnt_stride;
+      if (dbg && c.m_dbg >= 0) io.m_dbg = dbg + c.m_dbg;
+      const bool sparse = c.u < c.LQ;
+      if (a.mt_in) {
+        mt_replay<NTHREADS>(gen, c.LQ, c.U, c.LK, sparse ? reinterpret_cast<uint32_t*>(CNT) : nullptr,
+                            c.cnt_stride);
+        if (call == PL.n_calls - 1 && b == 0) mt_store<NTHREADS>(gen, a.mt_out);
+      } else if (sparse) {
+        const int bytes = ((c.LQ + 15) & ~15) * c.cnt_stride;
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + c.cnt_off);
+        f32x4* dst = reinterpret_cast<f32x4*>(CNT);
+        for (int i = threadIdx.x; i < bytes / 16; i += NTHREADS) dst[i] = src[i];
+        __syncthreads();
+      }
+      if (sparse) io.cnt = CNT;
+    }
+#ifndef V3_NO_ATTN
+    attention_head<MQ_, MK_>(io, M, w);
+#endif
+  };
+
+  for (int e = 0; e < PL.n_enc; ++e) {
+    stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);
+    __syncthreads();
+    // ---- DataEmbedding (embed.py:132-135) on the EncoderStack window x[:, -L:] (encoder.py:95-106)
+    int L = L0 >> e;
+    const int off = L0 - L;
+    int nmt = (L + 15) >> 4;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) X.v[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      const GemmDesc d = PL.emb_enc;
+      gemm_res<2, MT>(M, d, nmt, LoadEmbedOff{IN, L0, PL.C_shift, CS, off}, [&](int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_op() & 15);
+        const int prow = m + off < LMAX ? m + off : LMAX - 1;
+        X.v[mt] = y + pload4(M, PL.pe_enc, prow * DMODEL + n0);
+      });
+    }
+    __syncthreads();                       // IN (aliases CTX) fully read
+    store_res(X, nmt, L, Xb);
+    __syncthreads();
+    if (dbg && e == 0) dump_res(X, nmt, L, dbg + PL.dbg_emb);
+    STAMP();  // embedding
+
+    const int first = PL.enc_first[e];
+    for (int l = 0; l < PL.enc_layers[e]; ++l) {
+      L = ELD.L_in;
+      nmt = (L + 15) >> 4;
+      // ---- AttentionLayer + ProbAttention / FullAttention, one head per wave, context → CTX
+      {
+        const GemmDesc q = ELD.qkv;
+        attend(IC<MT>{}, IC<MT>{}, Xb, Xb, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+               part_of(q, 0), part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
+               a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
+      }
+      __syncthreads();
+      STAMP();  // encoder attention
+      {
+        const GemmDesc d = ELD.o;   // x = x + new_x (encoder.py:49)
+        gemm_res<4, MT>(M, d, nmt, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
+      }
+      FINE(l, 0);
+      ln_res(X, nmt, L, M, ELD.ln1, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      STAMP();  // out-projection + LN1
+      {
+        const GemmDesc d = ELD.f1;  // conv1 (k=1) + activation (encoder.py:52)
+        const int relu = PL.act_relu;
+        gemm_tiles<4>(M, d, DFF / 16, nmt, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
+          *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_op() & 15)) * BS + n0) = cvt4(v);
+        });
+      }
+      FINE(l, 1);
+      __syncthreads();
+      FINE(l, 2);
+      {
+        const GemmDesc d = ELD.f2;  // conv2 (k=1) + residual (encoder.py:53-56)
+        gemm_res<DFF / 32, MT>(M, d, nmt, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
+      }
+      FINE(l, 3);
+      ln_res(X, nmt, L, M, ELD.ln2, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      STAMP();  // FFN + LN2
+      if (dbg && ELD.dbg_layer >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_layer);
+      FINE(l, 4);
+#ifndef V3_NO_CONV
+      if (ELD.conv.n) {
+        // ---- ConvLayer (encoder.py:22-28): circular conv, BN(eval) folded, ELU, MaxPool(3,2,1).
+        // The conv output lives inside each m-tile-count instantiation and only X leaves it.
+        const GemmDesc d = ELD.conv;
+        with_nmt(nmt, [&](auto NMT) __attribute__((always_inline)) {
+          constexpr int N_ = decltype(NMT)::value;
+          Res<N_> Cv;
+          gemm_kouter_res<12, 4, N_>(M, d, LoadCirc3BF16{Xb, L},
+                                     [&](int mt, int n0, f32x4 v) __attribute__((always_inline)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
+            Cv.v[mt] = v;
+          });
+          FINE(l, 5);
+          maxpool_res<N_>(Cv, L, X);
+        });
+        FINE(l, 6);
+        L = ELD.L_out;
+        nmt = (L + 15) >> 4;
+        __syncthreads();                   // every wave finished reading Xb
+        FINE(l, 7);
+        store_res(X, nmt, L, Xb);
+        __syncthreads();
+        STAMP();  // distil conv + pool
+        if (dbg && ELD.dbg_conv >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_conv);
+      }
+#endif
+    }
+    // ---- Encoder.norm (encoder.py:83-84) → this encoder's rows of the stack output (ENC)
+    const int rows = PL.enc_rows[e];
+    ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, Xb,
+           ENC + PL.enc_row_off[e] * BS);
+    __syncthreads();
+    if (dbg && PL.enc_dbg[e] >= 0) dump_res(X, nmt, rows, dbg + PL.enc_dbg[e]);
+    STAMP();  // encoder norm
+  }
+
+  // ================================ decoder (decoder.py:43-56), instantiated for its compile-time
+  // tile count (dec_len ≤ 48)
+  const int Ld = PL.dec_len, S = PL.S;
+  stage(a.x_dec + (size_t)b * Ld * C, IN, Ld, C, CS);
+  __syncthreads();
+  auto decoder = [&](auto NMDc) __attribute__((always_inline)) {
+    constexpr int NMD = decltype(NMDc)::value;
+    const int nmd = NMD;
+    Res<NMD> XD;
+    {
+      const GemmDesc d = PL.emb_dec;
+      gemm_res_n<2, NMD>(M, d, LoadEmbedOff{IN, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_op() & 15);
+        const int prow = m < LMAX ? m : LMAX - 1;
+        XD.v[mt] = y + pload4(M, PL.pe_dec, prow * DMODEL + n0);
+      });
+    }
+    __syncthreads();
+    store_res(XD, nmd, Ld, Xb);
+    __syncthreads();
+    if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_emb);
+    STAMP();  // decoder embedding
+
+    for (int l = 0; l < PL.d_layers; ++l) {
+      {
+        // masked self-attention with the mix scramble (model.py:211-222)
+        const GemmDesc q = DLD.qkv;
+        attend(IC<NMD>{}, IC<NMD>{}, Xb, Xb, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+               part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld, PL.prob, 1, PL.mix, DLD.call, nullptr);
+      }
+      __syncthreads();
+      STAMP();  // decoder self-attention
+      {
+        const GemmDesc d = DLD.o;
+        gemm_res_n<4, NMD>(M, d, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      }
+      ln_res(XD, nmd, Ld, M, DLD.ln1, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      {
+        // cross-attention: FullAttention over the encoder-stack output, mix=False
+        const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
+        attend(IC<NMD>{}, IC<MT>{}, Xb, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+               part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
+      }
+      __syncthreads();
+      STAMP();  // cross-attention
+      {
+        const GemmDesc d = DLD.co;
+        gemm_res_n<4, NMD>(M, d, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      }
+      ln_res(XD, nmd, Ld, M, DLD.ln2, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      {
+        const GemmDesc d = DLD.f1;
+        const int relu = PL.act_relu;
+        gemm_tiles<4>(M, d, DFF / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
+          *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_op() & 15)) * BS + n0) = cvt4(v);
+        });
+      }
+      __syncthreads();
+      {
+        const GemmDesc d = DLD.f2;
+        gemm_res_n<DFF / 32, NMD>(M, d, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      }
+      ln_res(XD, nmd, Ld, M, DLD.ln3, 1e-5f, false, LNP, Xb);
+      __syncthreads();
+      STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3
+      if (dbg && DLD.dbg >= 0) dump_res(XD, nmd, Ld, dbg + DLD.dbg);
+    }
+    ln_res(XD, nmd, Ld, M, PL.dec_norm, 1e-5f, false, LNP, Xb);
+    __syncthreads();
+    if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_out);
+    {
+      // projection (model.py:264) on the last pred_len rows → out[b]
+      const GemmDesc d = PL.proj;
+      const int first_row = Ld - PL.pred_len, co = PL.c_out;
+      float* out = a.out + (size_t)b * PL.pred_len * co;
+      gemm_tiles<4>(M, d, d.n / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+        const int m = mt * 16 + (lane_op() & 15);
+        if (m < first_row || m >= Ld) return;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n0 + r < co) out[(m - first_row) * co + n0 + r] = v[r];
+      });
+    }
+    STAMP();  // final norm + projection
+  };
+#ifndef V3_NO_DEC
+  switch ((Ld + 15) >> 4) {
+    case 1: decoder(IC<1>{}); break;
+    case 2: decoder(IC<2>{}); break;
+    default: decoder(IC<3>{}); break;
+  }
+#endif
+}
+
+#undef PL
+#undef ELD
+#undef DLD
+
+}  // namespace v3
+}  // namespace cet
+
+extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
+  using namespace cet;
+  if (a->B <= 0) return 0;
+  auto launch = [&](auto kern) -> int {
+    static bool attr_done = false;
+    if (!attr_done) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024) != hipSuccess)
+        return -1;
+      attr_done = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(a->B), dim3(v3::NTHREADS), lds_bytes, stream, *a);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  };
+  switch (dff) {
+    case 64: return launch(v3::informer_forward_v3<64>);
+    case 128: return launch(v3::informer_forward_v3<128>);
+    default: return -3;
+  }
+}

@@ -67,6 +67,7 @@ struct TransformerArgs {
 
 extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);

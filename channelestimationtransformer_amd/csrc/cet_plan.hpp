@@ -23,7 +23,10 @@ constexpr int BS = 136;
 __host__ __device__ inline int cnt_word_off(int key) { return ((key >> 2) & 3) * 24 + (key >> 4) * 4; }
 __host__ __device__ inline int cnt_pos_v2(int key) { return cnt_word_off(key) + (key & 3); }
 // v2 per-wave attention scratch: 96 u64 selection keys | 96 int16 selected rows | 96 flag bytes
-constexpr int V2_SCR_FLOATS = 264;   // bf16 row stride (elements) of Q/K/ctx-like LDS buffers (+16 B per row)
+constexpr int V2_SCR_FLOATS = 264;
+// v3 LayerNorm partials: floats per row (8 waves × (mean, M2) + pad; 80-byte rows put 16
+// consecutive rows on distinct bank quads)
+constexpr int LN3_STRIDE = 20;
 
 // One dense layer: packed bf16 weights (fragment order) + fp32 epilogue vectors.
 struct GemmDesc {
@@ -88,6 +91,8 @@ struct InformerPlan {
   int vts;
   // v2 (register-resident) kernel LDS layout
   int lds2_XB, lds2_CTX, lds2_ENC, lds2_LN, lds2_SCR, lds2_CNT, lds2_MT, lds2_bytes;
+  // v3 (8-wave) layout: the LayerNorm partials alias the per-wave attention scratch
+  int lds3_XB, lds3_CTX, lds3_ENC, lds3_SCR, lds3_CNT, lds3_MT, lds3_bytes;
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
 };

@@ -235,7 +235,7 @@ def test_nmse_split_kernel(shape):
     np.testing.assert_allclose(acc.cpu().numpy(), 3 * ref_split(p, y), rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_kernel_variants_agree_with_oracle(variant):
     """Both fused-kernel generations (LDS-resident v1, register-resident v2) meet the bar."""
     _gpu()
