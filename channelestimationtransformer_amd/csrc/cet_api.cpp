@@ -126,6 +126,15 @@ struct cet_engine {
   void sync_host_rng() {
     for (; host_lag > 0; --host_lag) (void)rng.next();
   }
+  // v3 prepared tables: the multiplicity tables of the NEXT forward are built by the first
+  // workgroup of the current forward to finish (or by cet_launch_sampler_prep after a reseed),
+  // so no forward replays the stream on its critical path.  d_tab[tab_cur] holds the tables of
+  // the next forward when tab_ready; d_mt[mt_cur] is then the state after their draws.
+  uint8_t* d_tab[2] = {};
+  int tab_cur = 0;
+  bool tab_ready = false;
+  unsigned* d_ticket = nullptr;
+  static constexpr int PREP_MIN_B = 64;   // below this the first finisher has no slack to hide in
 
   // per-forward multiplicity tables (ring of pinned staging + device buffers)
   static constexpr int NSLOT = 4;
@@ -158,6 +167,9 @@ struct cet_engine {
       if (ev[i]) (void)hipEventDestroy(ev[i]);
     }
     if (d_mt) (void)hipFree(d_mt);
+    for (auto* t : d_tab)
+      if (t) (void)hipFree(t);
+    if (d_ticket) (void)hipFree(d_ticket);
     if (h_mt) (void)hipHostFree(h_mt);
     if (ev_mt) (void)hipEventDestroy(ev_mt);
   }
@@ -676,7 +688,14 @@ int upload(cet_engine* e) {
       HIP_TRY(hipMalloc((void**)&e->d_mt, 2 * 640 * sizeof(uint32_t)));
       HIP_TRY(hipHostMalloc((void**)&e->h_mt, 640 * sizeof(uint32_t)));
       HIP_TRY(hipEventCreateWithFlags(&e->ev_mt, hipEventDisableTiming));
+      HIP_TRY(hipMalloc((void**)&e->d_ticket, 64));
+      HIP_TRY(hipMemset(e->d_ticket, 0, 64));
     }
+    for (auto*& t : e->d_tab) {
+      if (t) HIP_TRY(hipFree(t));
+      HIP_TRY(hipMalloc((void**)&t, e->cnt_bytes));
+    }
+    e->tab_ready = false;
     e->draws_per_forward = 0;
     for (const auto& c : e->calls) e->draws_per_forward += (int64_t)c.LQ * c.U;
   }
@@ -1052,6 +1071,8 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.cnt = nullptr;
   a.mt_in = nullptr;
   a.mt_out = nullptr;
+  a.cnt_next = nullptr;
+  a.ticket = nullptr;
   a.x_enc = x_enc;
   a.x_dec = x_dec;
   a.out = out;
@@ -1070,10 +1091,37 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
       HIP_TRY(hipEventRecord(e->ev_mt, st));
       e->ev_mt_used = true;
       e->dev_mt_valid = true;
+      e->tab_ready = false;
     }
-    a.mt_in = e->d_mt + 640 * e->mt_cur;
-    a.mt_out = e->d_mt + 640 * (1 - e->mt_cur);
-    e->mt_cur = 1 - e->mt_cur;
+    const bool prep = e->variant == 3 && B >= cet_engine::PREP_MIN_B;
+    if (prep && !e->tab_ready) {
+      // first forward after a (re)seed: this forward's tables from a one-workgroup launch
+      const int lds = 640 * 4 + (p.lds3_MT - p.lds3_CNT);
+      if (cet_launch_sampler_prep((const InformerPlan*)e->d_plan, e->d_mt + 640 * e->mt_cur,
+                                  e->d_mt + 640 * (1 - e->mt_cur), e->d_tab[e->tab_cur], lds, st))
+        return fail(CET_E_HIP, std::string("sampler prep launch failed: ") + hipGetErrorString(hipGetLastError()));
+      e->mt_cur = 1 - e->mt_cur;
+      e->tab_ready = true;
+    }
+    if (e->tab_ready) {
+      // prepared tables: staged by this forward; a large one also prepares the next forward's
+      // (d_mt[mt_cur] is the state after this forward's draws)
+      a.cnt = e->d_tab[e->tab_cur];
+      if (prep) {
+        a.mt_in = e->d_mt + 640 * e->mt_cur;
+        a.mt_out = e->d_mt + 640 * (1 - e->mt_cur);
+        a.cnt_next = e->d_tab[1 - e->tab_cur];
+        a.ticket = e->d_ticket;
+        e->mt_cur = 1 - e->mt_cur;
+        e->tab_cur = 1 - e->tab_cur;
+      } else {
+        e->tab_ready = false;
+      }
+    } else {
+      a.mt_in = e->d_mt + 640 * e->mt_cur;
+      a.mt_out = e->d_mt + 640 * (1 - e->mt_cur);
+      e->mt_cur = 1 - e->mt_cur;
+    }
     e->host_lag += e->draws_per_forward;
     const int tk = timing_mark(e, st);
     rc = launch_fused(e, a, st);

@@ -6,6 +6,7 @@
 // attn.py:37-209, embed.py:8-135 (the v2 kernel, cet_informer2.hip, has the same phase order).
 #include "cet_kernels.h"
 #include "cet_mt.hpp"
+#include "cet_sampler.hpp"
 #include "cet_v3.hpp"
 
 namespace cet {
@@ -102,7 +103,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
       ++sid;
     }
   };
-  if (a.mt_in) {
+  if (a.mt_in && !a.cnt) {
     __syncthreads();   // LDS zeroing above is done before the state lands in it
     mt_load<NTHREADS>(gen, a.mt_in);
   }   // device-resident sampler (cet_mt.hpp)
@@ -128,7 +129,8 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
       io.cnt_stride = c.cnt_stride;
       if (dbg && c.m_dbg >= 0) io.m_dbg = dbg + c.m_dbg;
       const bool sparse = c.u < c.LQ;
-      if (a.mt_in) {
+      if (!a.cnt) {
+        // resident sampler: replay this call's draws into the LDS table (cet_mt.hpp)
         mt_replay<NTHREADS>(gen, c.LQ, c.U, c.LK, sparse ? reinterpret_cast<uint32_t*>(CNT) : nullptr,
                             c.cnt_stride);
         if (call == PL.n_calls - 1 && b == 0) mt_store<NTHREADS>(gen, a.mt_out);
@@ -346,6 +348,22 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
     default: decoder(IC<3>{}); break;
   }
 #endif
+  // ---- the first workgroup to finish prepares the NEXT forward's ProbSparse tables from the
+  //      resident sampler state (cet_sampler.hpp) while the rest of the grid drains; the last
+  //      one to finish re-arms the counter for the next launch
+  if (a.ticket) {
+    __syncthreads();
+    unsigned* tk = reinterpret_cast<unsigned*>(lds + PL.lds3_SCR);
+    if (threadIdx.x == 0) {
+      const unsigned t = atomicAdd(a.ticket, 1u);
+      if (t + 1u == (unsigned)a.B) atomicExch(a.ticket, 0u);
+      *tk = t;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(*tk) == 0u && a.cnt_next)
+      replay_all<NTHREADS>(PL, a.mt_in, a.mt_out, a.cnt_next, reinterpret_cast<uint32_t*>(lds + PL.lds3_MT),
+                           reinterpret_cast<uint32_t*>(lds + PL.lds3_CNT));
+  }
 }
 
 #undef PL
@@ -374,4 +392,23 @@ extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int l
     case 128: return launch(v3::informer_forward_v3<128>);
     default: return -3;
   }
+}
+
+namespace cet {
+namespace v3 {
+// One-workgroup table preparation for the first forward after a (re)seed.
+__global__ void __launch_bounds__(NTHREADS) sampler_prep(const InformerPlan* plan, const uint32_t* mt_in,
+                                                         uint32_t* mt_out, uint8_t* tab_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  replay_all<NTHREADS>(*plan, mt_in, mt_out, tab_out, reinterpret_cast<uint32_t*>(lds),
+                       reinterpret_cast<uint32_t*>(lds + MT_WORDS * 4));
+}
+}  // namespace v3
+}  // namespace cet
+
+extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
+                                       uint8_t* tab_out, int lds_bytes, hipStream_t stream) {
+  hipLaunchKernelGGL(cet::v3::sampler_prep, dim3(1), dim3(cet::v3::NTHREADS), lds_bytes, stream, plan, mt_in, mt_out,
+                     tab_out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }

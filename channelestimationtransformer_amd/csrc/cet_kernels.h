@@ -16,6 +16,8 @@ struct InformerArgs {
   const uint8_t* cnt;         // per-forward ProbSparse key multiplicities (host-built), or
   const uint32_t* mt_in;      // v2: resident mt19937 state slot to replay the draws from, and
   uint32_t* mt_out;           //     the slot workgroup 0 writes the advanced state to
+  uint8_t* cnt_next;          // v3: where the first workgroup to finish writes the next forward's tables
+  unsigned* ticket;           // v3: finish counter for that election (the last finisher re-arms it)
   const float* x_enc;         // [B][seq_len][C]
   const float* x_dec;         // [B][dec_len][C]
   float* out;                 // [B][pred_len][c_out]
@@ -67,6 +69,8 @@ struct TransformerArgs {
 
 extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
+                                       uint8_t* tab_out, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);

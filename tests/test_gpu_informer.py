@@ -156,6 +156,46 @@ def test_resident_sampler_continues_the_stream():
         np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{j + 1}")
 
 
+def test_prepared_tables_continue_the_stream():
+    """v3 at B >= 64 stages tables prepared ahead (by the previous forward's first workgroup to
+    finish, or a prep launch after a reseed).  Interleaved with small forwards (in-kernel replay,
+    or the pending prepared tables) and a host draw, every forward must consume exactly the draws
+    torch.randint would, in order (bitwise against explicit-index runs)."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case("informer_prob_b4")
+    m = model_for(case)
+    dev = torch.device("cuda:0")
+    eng = m.engine(dev)
+    xe_np = np.ascontiguousarray(np.tile(case.z["x_enc"], (32, 1, 1)))
+    xd_np = np.ascontiguousarray(np.tile(case.z["x_dec"], (32, 1, 1)))
+    xe, xd = torch.from_numpy(xe_np).to(dev), torch.from_numpy(xd_np).to(dev)
+    seed = 777
+    shapes = eng.prob_calls()
+    torch.manual_seed(seed)
+    plan = [128, 128, 4, 4, 128, 0, 128, 128]   # forward batch sizes in order; 0 = a host draw
+    draws = [[torch.randint(lk, shp).numpy() for lk, shp in shapes] for _ in plan]
+    eng.seed(seed)
+    outs = []
+    for i, B in enumerate(plan):
+        if B == 0:
+            for g, r in zip(eng.native_draw(), draws[i]):
+                np.testing.assert_array_equal(g, r)
+            outs.append(None)
+            continue
+        o = torch.empty(B, 5, 16, device=dev)
+        eng.forward(xe[:B].contiguous(), xd[:B].contiguous(), o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        if o is None:
+            continue
+        B = o.shape[0]
+        ref, _, _ = run_engine(m, xe_np[:B], xd_np[:B], draws[i])
+        np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{i + 1} (B={B})")
+
+
 def test_batch_sharding_is_bitwise_per_sequence():
     """Every sequence is independent: a batch split in shards gives bitwise-identical rows."""
     _gpu()
