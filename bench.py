@@ -75,14 +75,17 @@ def cpu_baseline(seconds: float = 12.0, batch: int = 32):
             "sample": f"{n} forwards of B={batch} (numpy oracle, float32, {dt:.1f}s)"}
 
 
-def load_traffic(profile_dir):
-    """HBM bytes per launch of the fused kernel from a committed rocprofv3 PMC summary, if any."""
+def load_traffic(profile_dir, kernel):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary (None if the summary
+    was collected on another kernel variant)."""
     path = os.path.join(profile_dir, "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
+        if kernel not in (d.get("kernel") or ""):
+            return None
         return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
@@ -210,7 +213,7 @@ def main():
             "parity_rel_nmse_vs_oracle": parity,
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
-                         "traffic": load_traffic(os.path.join(ROOT, "profiles")),
+                         "traffic": load_traffic(os.path.join(ROOT, "profiles"), KERNEL_NAMES[args.variant]),
                          "kernel": KERNEL_NAMES[args.variant], "kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
