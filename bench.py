@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--variant", type=int, default=3,
                     help="fused-kernel generation (1: LDS-resident, 2: 4-wave register-resident, 3: 8-wave)")
+    ap.add_argument("--sampler", choices=("device", "host"), default="device",
+                    help="where the native ProbSparse draws run (identical streams; DESIGN §3.3)")
     args = ap.parse_args()
 
     import torch
@@ -127,6 +129,7 @@ def main():
     model = build_model(dev)
     eng = model.engine(dev)
     eng.set_variant(args.variant)
+    eng.set_sampler(args.sampler == "host")
     eng.seed(1)                 # every rank draws the same index samples (shared across the batch)
     B = args.batch
     xe_np, xd_np, lab_np = make_batch(B, snr=args.snr, seed=1234 + 7919 * rank)

@@ -55,6 +55,7 @@ def _load():
         "cet_nmse_split": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p]),
         "cet_timing": (c_int, [c_void_p, c_int]),
         "cet_set_variant": (c_int, [c_void_p, c_int]),
+        "cet_set_sampler": (c_int, [c_void_p, c_int]),
         "cet_set_stamps": (c_int, [c_void_p, c_void_p]),
         "cet_timing_read": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
         "cet_prepare_batch": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p,
@@ -76,7 +77,7 @@ EXPORTED = ("cet_last_error", "cet_version", "cet_create_informer", "cet_create_
             "cet_native_draw",
             "cet_forward", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
             "cet_debug_layout", "cet_nmse_split", "cet_timing", "cet_timing_read",
-            "cet_set_variant", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
+            "cet_set_variant", "cet_set_sampler", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
 
 
 def check(rc: int, what: str = "") -> int:

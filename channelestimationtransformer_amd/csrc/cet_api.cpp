@@ -111,6 +111,7 @@ struct cet_engine {
   std::vector<std::vector<int32_t>> idx;
   std::vector<bool> idx_set;
   bool native_rng = false;
+  bool host_sampler = false;   // cet_set_sampler: native draws on the host, tables staged per forward
   MT19937 rng;
   // device-resident copy of the same stream (v2 kernel, cet_mt.hpp): two HBM slots of
   // 624 words + read index; the kernel reads slot mt_cur and writes the advanced state to the
@@ -1080,7 +1081,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.dbg = e->dbg;
   a.stamps = e->stamps;
   a.B = B;
-  if (e->variant >= 2 && e->native_rng && p.n_calls) {
+  if (e->variant >= 2 && e->native_rng && p.n_calls && !e->host_sampler) {
     // ---- resident sampler: the kernel replays this forward's draws itself (cet_mt.hpp)
     if (!e->dev_mt_valid) {
       e->sync_host_rng();
@@ -1177,6 +1178,13 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   e->stamps = reinterpret_cast<unsigned long long*>(stamps_dev);
+  return CET_OK;
+}
+
+int cet_set_sampler(cet_engine* e, int on_host) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (on_host != 0 && on_host != 1) return fail(CET_E_INVALID, "on_host must be 0 or 1");
+  e->host_sampler = on_host != 0;
   return CET_OK;
 }
 

@@ -66,7 +66,9 @@ __device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
   return d;
 }
 
-template <int DFF>
+// DIAG: the instance that honours the optional outputs (attns maps, activation dump, phase stamps);
+// the production instance compiles them out, which frees the scalar registers their pointers held.
+template <int DFF, bool DIAG>
 __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(a.plan))
@@ -85,7 +87,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   MTState gen{reinterpret_cast<uint32_t*>(lds + PL.lds3_MT), MT_N};
   float* SCR = reinterpret_cast<float*>(lds + PL.lds3_SCR) + w * V2_SCR_FLOATS;
   float* IN = reinterpret_cast<float*>(lds + PL.lds3_CTX);      // staged raw input (aliases CTX)
-  float* dbg = a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
+  float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
 
   // zero the activation images: rows past L of Xb / CTX / ENC are read (never used) by MFMAs
   for (int i = threadIdx.x; i < PL.lds3_CNT / 16; i += NTHREADS)
@@ -95,7 +97,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // bf16x8 per n-tile at K = 128
   Res<MT> X;
   // diagnostics: s_memtime at phase boundaries (wave 0, lane 0), off unless a.stamps is set
-  unsigned long long* stamps = a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
+  unsigned long long* stamps = DIAG && a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
   int sid = 0;
   auto STAMP = [&]() {
     if (stamps) {
@@ -180,7 +182,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
         const GemmDesc q = ELD.qkv;
         attend(IC<MT>{}, IC<MT>{}, Xb, Xb, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
                part_of(q, 0), part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
-               a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
+               DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
       }
       __syncthreads();
       STAMP();  // encoder attention
@@ -376,20 +378,21 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
 extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
   using namespace cet;
   if (a->B <= 0) return 0;
-  auto launch = [&](auto kern) -> int {
-    static bool attr_done = false;
-    if (!attr_done) {
+  static bool attr_done[4] = {false, false, false, false};   // one flag per kernel instance
+  auto launch = [&](void (*kern)(InformerArgs), int slot) -> int {
+    if (!attr_done[slot]) {
       if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024) != hipSuccess)
         return -1;
-      attr_done = true;
+      attr_done[slot] = true;
     }
     hipLaunchKernelGGL(kern, dim3(a->B), dim3(v3::NTHREADS), lds_bytes, stream, *a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   };
+  const bool diag = a->attns || a->dbg || a->stamps;
   switch (dff) {
-    case 64: return launch(v3::informer_forward_v3<64>);
-    case 128: return launch(v3::informer_forward_v3<128>);
+    case 64: return diag ? launch(v3::informer_forward_v3<64, true>, 0) : launch(v3::informer_forward_v3<64, false>, 1);
+    case 128: return diag ? launch(v3::informer_forward_v3<128, true>, 2) : launch(v3::informer_forward_v3<128, false>, 3);
     default: return -3;
   }
 }

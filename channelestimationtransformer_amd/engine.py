@@ -117,6 +117,10 @@ class Engine:
         """Diagnostics: per-phase s_memtime stamps into an int64 device tensor of B·128 (or None)."""
         check(lib.cet_set_stamps(self._h, ctypes.c_void_p(buf.data_ptr()) if buf is not None else None))
 
+    def set_sampler(self, on_host: bool) -> None:
+        """Native ProbSparse draws on the host (True) or the device-resident sampler (False)."""
+        check(lib.cet_set_sampler(self._h, int(bool(on_host))), "cet_set_sampler")
+
     def set_variant(self, variant: int) -> None:
         """Fused-kernel generation: 2 (register-resident, default) or 1 (LDS-resident)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")

@@ -102,10 +102,18 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen);
 /* Diagnostics (v2 kernel): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
 
-/* Select the fused-kernel generation of an Informer engine: 2 (default, register-resident,
- * two sequences per CU) or 1 (LDS-resident, one sequence per CU).  CET_KERNEL=v1 in the
- * environment selects 1 at creation. */
+/* Select the fused-kernel generation of an Informer engine: 3 (default, 8-wave register-resident,
+ * two sequences per CU), 2 (4-wave register-resident) or 1 (LDS-resident, one sequence per CU).
+ * CET_KERNEL=v1 in the environment selects 1 at creation. */
 int cet_set_variant(cet_engine* e, int variant);
+
+/* Where the native sampler (after cet_seed) runs for variants 2/3: 0 = on the device (the
+ * resident mt19937, default), 1 = on the host (the same torch-compatible stream drawn by the host
+ * mirror, the multiplicity tables staged per forward through a pinned ring and copied on the
+ * caller's stream ahead of the kernel).  Both give identical draws; switching keeps the stream.
+ * Replaces nothing in the reference: there the draw is torch.randint on the CPU
+ * (FullPrecision/InformerModel/attn.py:96-98), which is what on_host = 1 mirrors. */
+int cet_set_sampler(cet_engine* e, int on_host);
 
 /* Kernel timing: when enabled, every cet_forward brackets its kernel launch with a pair of
  * hipEvents on the caller's stream; cet_timing_read() waits for them and returns the summed

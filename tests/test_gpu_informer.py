@@ -196,6 +196,40 @@ def test_prepared_tables_continue_the_stream():
         np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{i + 1} (B={B})")
 
 
+def test_host_and_device_samplers_share_the_stream():
+    """cet_set_sampler switches the native draws between the device-resident mt19937 and the host
+    mirror mid-stream (with prepared tables pending); every forward still consumes exactly the
+    draws torch.randint would (bitwise against explicit-index runs)."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case("informer_prob_b4")
+    m = model_for(case)
+    dev = torch.device("cuda:0")
+    eng = m.engine(dev)
+    xe_np = np.ascontiguousarray(np.tile(case.z["x_enc"], (32, 1, 1)))
+    xd_np = np.ascontiguousarray(np.tile(case.z["x_dec"], (32, 1, 1)))
+    xe, xd = torch.from_numpy(xe_np).to(dev), torch.from_numpy(xd_np).to(dev)
+    seed = 31337
+    shapes = eng.prob_calls()
+    torch.manual_seed(seed)
+    plan = [("dev", 128), ("dev", 128), ("host", 128), ("host", 4), ("dev", 128), ("host", 128), ("dev", 4)]
+    draws = [[torch.randint(lk, shp).numpy() for lk, shp in shapes] for _ in plan]
+    eng.seed(seed)
+    outs = []
+    for where, B in plan:
+        eng.set_sampler(where == "host")
+        o = torch.empty(B, 5, 16, device=dev)
+        eng.forward(xe[:B].contiguous(), xd[:B].contiguous(), o)
+        outs.append(o)
+    eng.set_sampler(False)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        B = o.shape[0]
+        ref, _, _ = run_engine(m, xe_np[:B], xd_np[:B], draws[i])
+        np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{i + 1} ({plan[i]})")
+
+
 def test_batch_sharding_is_bitwise_per_sequence():
     """Every sequence is independent: a batch split in shards gives bitwise-identical rows."""
     _gpu()

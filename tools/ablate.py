@@ -46,8 +46,12 @@ def main():
         eng.set_variant(v)
         eng.seed(1)
         t_res = run(eng, xe, xd, out, None)
+        eng.set_sampler(True)
+        t_nh = run(eng, xe, xd, out, None)
+        eng.set_sampler(False)
         t_host = run(eng, xe, xd, out, idx)
-        print(f"variant {v}: resident sampler {t_res:8.1f} us   host tables {t_host:8.1f} us", flush=True)
+        print(f"variant {v}: resident sampler {t_res:8.1f} us   native host sampler {t_nh:8.1f} us   "
+              f"host tables {t_host:8.1f} us", flush=True)
 
 
 if __name__ == "__main__":
