@@ -10,7 +10,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int64, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcet.so")
+LIB_PATH = os.environ.get("CET_LIB") or os.path.join(HERE, "libcet.so")   # CET_LIB: an A/B build
 
 
 class CetError(RuntimeError):

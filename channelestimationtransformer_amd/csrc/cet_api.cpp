@@ -576,6 +576,8 @@ int build_informer(cet_engine* e) {
   }
   js << "]}";
   p.cnt_bytes = coff;
+  p.draws = 0;
+  for (int k = 0; k < p.n_calls; ++k) p.draws += p.calls[k].LQ * p.calls[k].U;
   e->cnt_bytes = coff ? coff : 16;
   p.dbg_stride = (int)dbg;
   e->dbg_json = js.str();
@@ -615,13 +617,16 @@ int build_informer(cet_engine* e) {
   // v3: bf16 image | context/FFN hidden/staged input | stack output | 8 waves' attention scratch,
   // aliased by the LayerNorm partials | multiplicity table | sampler state (≤ 80 KB: 2 per CU)
   o = 0;
-  p.lds3_XB = o; o = al(o + LP * BS * 2);
-  p.lds3_CTX = o; o = al(o + std::max(LP * BS * 2, LP * p.in_stride * 4));
-  p.lds3_ENC = o; o = al(o + SP * BS * 2);
-  p.lds3_SCR = o; o = al(o + std::max(LP * LN3_STRIDE * 4, 8 * V2_SCR_FLOATS * 4));
-  p.lds3_CNT = o; o = al(o + max_cnt);
-  p.lds3_MT = o; o = al(o + 624 * 4);
-  p.lds3_bytes = o;
+  // (fixed layout, cet_plan.hpp V3L_*: only the stack output's size depends on the plan)
+  if (LMAX * p.in_stride * 4 > V3L_SCR - V3L_CTX || max_cnt > V3L_MT - V3L_CNT || LP > LMAX)
+    return fail(CET_E_INVALID, "v3 LDS layout: staged input or multiplicity table exceeds its region");
+  p.lds3_XB = V3L_XB;
+  p.lds3_CTX = V3L_CTX;
+  p.lds3_SCR = V3L_SCR;
+  p.lds3_CNT = V3L_CNT;
+  p.lds3_MT = V3L_MT;
+  p.lds3_ENC = V3L_ENC;
+  p.lds3_bytes = al(V3L_ENC + SP * BS * 2);
   return CET_OK;
 }
 
@@ -1097,7 +1102,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     const bool prep = e->variant == 3 && B >= cet_engine::PREP_MIN_B;
     if (prep && !e->tab_ready) {
       // first forward after a (re)seed: this forward's tables from a one-workgroup launch
-      const int lds = 640 * 4 + (p.lds3_MT - p.lds3_CNT);
+      const int lds = std::max(640 * 4 + (p.lds3_MT - p.lds3_CNT), std::min(replay_fast_lds(p), 64 * 1024));
       if (cet_launch_sampler_prep((const InformerPlan*)e->d_plan, e->d_mt + 640 * e->mt_cur,
                                   e->d_mt + 640 * (1 - e->mt_cur), e->d_tab[e->tab_cur], lds, st))
         return fail(CET_E_HIP, std::string("sampler prep launch failed: ") + hipGetErrorString(hipGetLastError()));

@@ -95,7 +95,28 @@ struct InformerPlan {
   int lds3_XB, lds3_CTX, lds3_ENC, lds3_SCR, lds3_CNT, lds3_MT, lds3_bytes;
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
+  int draws;                // mt19937 words one forward consumes (Σ LQ·U over every call)
 };
+
+// v3 LDS layout, fixed at compile time for every plan (LMAX rows; the kernel folds the offsets into
+// its ds_* immediates and keeps no LDS base in scalar registers): bf16 image | context / FFN hidden /
+// staged input | 8 waves' attention scratch aliased by the LayerNorm partials | multiplicity table |
+// sampler state | encoder-stack output (S rows, the only plan-sized region, last).
+constexpr int V3L_XB = 0;
+constexpr int V3L_CTX = V3L_XB + LMAX * BS * 2;
+constexpr int V3L_SCR = V3L_CTX + LMAX * BS * 2;
+constexpr int V3L_CNT = V3L_SCR + (LMAX * LN3_STRIDE * 4 > 8 * V2_SCR_FLOATS * 4 ? LMAX * LN3_STRIDE * 4
+                                                                                 : 8 * V2_SCR_FLOATS * 4);
+constexpr int V3L_MT = V3L_CNT + LMAX * 96;
+constexpr int V3L_ENC = V3L_MT + ((624 * 4 + 15) & ~15);
+static_assert(V3L_CTX % 16 == 0 && V3L_SCR % 16 == 0 && V3L_CNT % 16 == 0 && V3L_ENC % 16 == 0, "16-B regions");
+
+// LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded
+// mt19937 state | the forward's tempered words | every call's multiplicity table.
+constexpr int REPLAY_STATE_WORDS = 640;
+__host__ __device__ inline int replay_fast_lds(const InformerPlan& pl) {
+  return REPLAY_STATE_WORDS * 4 + ((pl.draws * 4 + 15) & ~15) + (int)pl.cnt_bytes;
+}
 
 struct TransformerPlan {
   int C, c_out, src_len, tgt_len, pred_len, N, dff;

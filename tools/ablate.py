@@ -50,6 +50,9 @@ def main():
         t_nh = run(eng, xe, xd, out, None)
         eng.set_sampler(False)
         t_host = run(eng, xe, xd, out, idx)
+        eng.seed(1)
+        t_res2 = run(eng, xe, xd, out, None)
+        print(f"variant {v}: resident sampler again {t_res2:8.1f} us", flush=True)
         print(f"variant {v}: resident sampler {t_res:8.1f} us   native host sampler {t_nh:8.1f} us   "
               f"host tables {t_host:8.1f} us", flush=True)
 
