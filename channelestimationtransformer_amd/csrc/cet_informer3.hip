@@ -204,47 +204,52 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
                part_of(q, 0), part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
                DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
       }
+      const WPre<4> po = prefetch_res<4>(M, ELD.o);   // x = x + new_x (encoder.py:49)
       __syncthreads();
       STAMP();  // encoder attention
-      {
-        const GemmDesc d = ELD.o;   // x = x + new_x (encoder.py:49)
-        gemm_res<4, MT>(M, d, nmt, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
-      }
+      gemm_res<4, MT>(po, nmt, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
       FINE(l, 0);
+      static_assert(DFF / 16 <= NW, "FFN hidden n-tiles: at most one per wave");
+      const WPre<4> pf1 = prefetch_tiles<4>(M, ELD.f1, DFF / 16);   // conv1 (k=1) + activation (encoder.py:52)
       ln_res(X, nmt, L, M, ELD.ln1, 1e-5f, false, LNP, Xb);
       __syncthreads();
       STAMP();  // out-projection + LN1
       {
-        const GemmDesc d = ELD.f1;  // conv1 (k=1) + activation (encoder.py:52)
         const int relu = PL.act_relu;
-        gemm_tiles<4>(M, d, DFF / 16, nmt, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+        gemm_tiles1<4>(pf1, DFF / 16, nmt, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
           *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_op() & 15)) * BS + n0) = cvt4(v);
         });
       }
       FINE(l, 1);
+      const WPre<DFF / 32> pf2 = prefetch_res<DFF / 32>(M, ELD.f2);  // conv2 (k=1) + residual (encoder.py:53-56)
       __syncthreads();
       FINE(l, 2);
-      {
-        const GemmDesc d = ELD.f2;  // conv2 (k=1) + residual (encoder.py:53-56)
-        gemm_res<DFF / 32, MT>(M, d, nmt, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
-      }
+      gemm_res<DFF / 32, MT>(pf2, nmt, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
       FINE(l, 3);
+      const int has_conv = ELD.conv.n;
+#ifdef V3_PREFETCH_CONV
+      WPre<4> pcv;
+      if (has_conv) pcv = prefetch_kouter<12, 4>(M, ELD.conv);
+#endif
       ln_res(X, nmt, L, M, ELD.ln2, 1e-5f, false, LNP, Xb);
       __syncthreads();
       STAMP();  // FFN + LN2
       if (dbg && ELD.dbg_layer >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_layer);
       FINE(l, 4);
 #ifndef V3_NO_CONV
-      if (ELD.conv.n) {
+      if (has_conv) {
         // ---- ConvLayer (encoder.py:22-28): circular conv, BN(eval) folded, ELU, MaxPool(3,2,1).
         // The conv output lives inside each m-tile-count instantiation and only X leaves it.
         const GemmDesc d = ELD.conv;
         with_nmt(nmt, [&](auto NMT) __attribute__((always_inline)) {
           constexpr int N_ = decltype(NMT)::value;
           Res<N_> Cv;
-          gemm_kouter_res<12, 4, N_>(M, d, LoadCirc3BF16{Xb, L},
+#ifndef V3_PREFETCH_CONV
+          const WPre<4> pcv = prefetch_kouter<12, 4>(M, d);
+#endif
+          gemm_kouter_res<12, 4, N_>(pcv, M, d, LoadCirc3BF16{Xb, L},
                                      [&](int mt, int n0, f32x4 v) __attribute__((always_inline)) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
@@ -304,12 +309,10 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
         attend(IC<NMD>{}, IC<NMD>{}, Xb, Xb, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
                part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld, PL.prob, 1, PL.mix, DLD.call, nullptr);
       }
+      const WPre<4> po = prefetch_res<4>(M, DLD.o);
       __syncthreads();
       STAMP();  // decoder self-attention
-      {
-        const GemmDesc d = DLD.o;
-        gemm_res_n<4, NMD>(M, d, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
-      }
+      gemm_res_n<4, NMD>(po, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
       ln_res(XD, nmd, Ld, M, DLD.ln1, 1e-5f, false, LNP, Xb);
       __syncthreads();
       {
@@ -318,12 +321,10 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
         attend(IC<NMD>{}, IC<MT>{}, Xb, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
                part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
       }
+      const WPre<4> pco = prefetch_res<4>(M, DLD.co);
       __syncthreads();
       STAMP();  // cross-attention
-      {
-        const GemmDesc d = DLD.co;
-        gemm_res_n<4, NMD>(M, d, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
-      }
+      gemm_res_n<4, NMD>(pco, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
       ln_res(XD, nmd, Ld, M, DLD.ln2, 1e-5f, false, LNP, Xb);
       __syncthreads();
       {
@@ -335,11 +336,9 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
           *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_op() & 15)) * BS + n0) = cvt4(v);
         });
       }
+      const WPre<DFF / 32> pf2 = prefetch_res<DFF / 32>(M, DLD.f2);
       __syncthreads();
-      {
-        const GemmDesc d = DLD.f2;
-        gemm_res_n<DFF / 32, NMD>(M, d, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
-      }
+      gemm_res_n<DFF / 32, NMD>(pf2, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
       ln_res(XD, nmd, Ld, M, DLD.ln3, 1e-5f, false, LNP, Xb);
       __syncthreads();
       STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3

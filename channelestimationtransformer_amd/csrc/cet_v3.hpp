@@ -76,38 +76,51 @@ struct Res {
   f32x4 v[N];
 };
 
+// A dense layer's per-wave operands — the KS weight fragments of n-tile w and the epilogue
+// vectors — requested ahead of time: callers issue them before the workgroup barrier that
+// precedes the layer, so their L2 latency overlaps the barrier wait instead of following it.
+template <int KS>
+struct WPre {
+  bf16x8 a[KS];
+  f32x4 sc, bi;
+};
+template <int KS>
+__device__ __forceinline__ WPre<KS> prefetch_res(const Mem& m, const GemmDesc d) {
+  WPre<KS> p;
+  const int lane = lane_op(), w = wave_id();
+  load_frags<KS>(m, d.w, w, p.a);
+  epi_vecs(m, d, 16 * w + (lane >> 4) * 4, p.sc, p.bi);
+  return p;
+}
+
 // Dense layer whose output n-tile w lands in the wave's residual fragments.
 // epi(mt, n0, f32x4 y) receives the finished (scaled, biased) value.
 template <int KS, int N, class BL, class Epi>
-__device__ __forceinline__ void gemm_res(const Mem& m, const GemmDesc d, int nmt, BL&& bl, Epi&& epi) {
+__device__ __forceinline__ void gemm_res(const WPre<KS>& p, int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_op(), w = wave_id();
-  bf16x8 a[KS];
-  load_frags<KS>(m, d.w, w, a);
   const int n0 = 16 * w + (lane >> 4) * 4;
-  f32x4 sc, bi;
-  epi_vecs(m, d, n0, sc, bi);
   const int kq = (lane >> 4) * 8, mrow = lane & 15;
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
-      epi(mt, n0, c * sc + bi);
+      for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+      epi(mt, n0, c * p.sc + p.bi);
     }
   }
+}
+template <int KS, int N, class BL, class Epi>
+__device__ __forceinline__ void gemm_res(const Mem& m, const GemmDesc d, int nmt, BL&& bl, Epi&& epi) {
+  gemm_res<KS, N>(prefetch_res<KS>(m, d), nmt, bl, epi);
 }
 
 // Compile-time m-tile count: no per-tile branch, B fragments of tile mt+1 requested before the
 // MFMAs of tile mt.
 template <int KS, int NMT, class BL, class Epi>
-__device__ __forceinline__ void gemm_res_n(const Mem& m, const GemmDesc d, BL&& bl, Epi&& epi) {
+__device__ __forceinline__ void gemm_res_n(const WPre<KS>& p, BL&& bl, Epi&& epi) {
   const int lane = lane_op(), w = wave_id();
-  bf16x8 a[KS];
-  load_frags<KS>(m, d.w, w, a);
   const int n0 = 16 * w + (lane >> 4) * 4;
-  f32x4 sc, bi;
-  epi_vecs(m, d, n0, sc, bi);
   const int kq = (lane >> 4) * 8, mrow = lane & 15;
   bf16x8 b[KS];
 #pragma unroll
@@ -121,13 +134,17 @@ __device__ __forceinline__ void gemm_res_n(const Mem& m, const GemmDesc d, BL&& 
     }
     f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(a[ks], b[ks], c);
-    epi(mt, n0, c * sc + bi);
+    for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(p.a[ks], b[ks], c);
+    epi(mt, n0, c * p.sc + p.bi);
     if (mt + 1 < NMT) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) b[ks] = bn[ks];
     }
   }
+}
+template <int KS, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_res_n(const Mem& m, const GemmDesc d, BL&& bl, Epi&& epi) {
+  gemm_res_n<KS, NMT>(prefetch_res<KS>(m, d), bl, epi);
 }
 
 // Dense layer over an arbitrary n-tile count (FFN hidden, projection), output through epi only.
@@ -162,17 +179,55 @@ __device__ __forceinline__ void gemm_tiles(const Mem& m, const GemmDesc d, int n
   }
 }
 
+// gemm_tiles for n_tiles ≤ NW (every wave owns at most one n-tile, so its operands can be
+// prefetched): wave w takes n-tile w mod n_tiles and every (NW / n_tiles)-th m-tile from w / n_tiles.
+template <int KS>
+__device__ __forceinline__ WPre<KS> prefetch_tiles(const Mem& m, const GemmDesc d, int n_tiles) {
+  WPre<KS> p;
+  const int lane = lane_op(), w = wave_id();
+  const int nt = w % n_tiles;
+  load_frags<KS>(m, d.w, nt, p.a);
+  epi_vecs(m, d, nt * 16 + (lane >> 4) * 4, p.sc, p.bi);
+  return p;
+}
+template <int KS, class BL, class Epi>
+__device__ __forceinline__ void gemm_tiles1(const WPre<KS>& p, int n_tiles, int nmt, BL&& bl, Epi&& epi) {
+  const int lane = lane_op(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int per = NW / n_tiles;
+  if (w >= per * n_tiles) return;
+  const int nt = w % n_tiles, mt_step = per;
+  const int n0 = nt * 16 + (lane >> 4) * 4;
+  for (int mt = w / n_tiles; mt < nmt; mt += mt_step) {
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) c = mfma16x16x32(p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+    epi(mt, n0, c * p.sc + p.bi);
+  }
+}
+
 // Deep-K dense layer (the distil conv, K = 384) in k-outer order with a compile-time m-tile count:
 // one accumulator per m-tile, the B fragments of step ks+1 requested before step ks's MFMAs, and
 // the weight fragments loaded in halves of KH k-steps (keeps the wave under 128 VGPRs).
+// The first KH of KS k-steps of n-tile w and the epilogue vectors of a deep-K layer.
+template <int KS, int KH>
+__device__ __forceinline__ WPre<KH> prefetch_kouter(const Mem& m, const GemmDesc d) {
+  WPre<KH> p;
+  const int lane = lane_op(), w = wave_id();
+#pragma unroll
+  for (int ks = 0; ks < KH; ++ks) p.a[ks] = wfrag(m, d.w * 16u + (uint32_t)(w * KS + ks) * 1024u, lane);
+  epi_vecs(m, d, 16 * w + (lane >> 4) * 4, p.sc, p.bi);
+  return p;
+}
+// `p` holds the first KH k-steps' fragments and the epilogue vectors (prefetch_kouter).
 template <int KS, int KH, int NMT, class BL, class Epi>
-__device__ __forceinline__ void gemm_kouter_res(const Mem& m, const GemmDesc d, BL&& bl, Epi&& epi) {
+__device__ __forceinline__ void gemm_kouter_res(const WPre<KH>& p, const Mem& m, const GemmDesc d, BL&& bl,
+                                                Epi&& epi) {
   static_assert(KS % KH == 0, "k-steps split into equal halves");
   const int lane = lane_op(), w = wave_id();
   const int kq = (lane >> 4) * 8, mrow = lane & 15;
   const int n0 = 16 * w + (lane >> 4) * 4;
-  f32x4 sc, bi;
-  epi_vecs(m, d, n0, sc, bi);
+  const f32x4 sc = p.sc, bi = p.bi;
   f32x4 c[NMT];
   bf16x8 b[NMT];
 #pragma unroll
@@ -185,7 +240,8 @@ __device__ __forceinline__ void gemm_kouter_res(const Mem& m, const GemmDesc d, 
   for (int hf = 0; hf < KS / KH; ++hf) {
     bf16x8 a[KH];
 #pragma unroll
-    for (int ks = 0; ks < KH; ++ks) a[ks] = wfrag(m, t0 + (uint32_t)(hf * KH + ks) * 1024u, lane);
+    for (int ks = 0; ks < KH; ++ks)
+      a[ks] = hf == 0 ? p.a[ks] : wfrag(m, t0 + (uint32_t)(hf * KH + ks) * 1024u, lane);
 #pragma unroll
     for (int ks = 0; ks < KH; ++ks) {
       const int kk = hf * KH + ks;
