@@ -618,7 +618,8 @@ int build_informer(cet_engine* e) {
   // aliased by the LayerNorm partials | multiplicity table | sampler state (≤ 80 KB: 2 per CU)
   o = 0;
   // (fixed layout, cet_plan.hpp V3L_*: only the stack output's size depends on the plan)
-  if (LMAX * p.in_stride * 4 > V3L_SCR - V3L_CTX || max_cnt > V3L_MT - V3L_CNT || LP > LMAX)
+  if (LMAX * p.in_stride * 4 > V3L_SCR - V3L_CTX || max_cnt > V3L_MT - V3L_CNT || LP > LMAX ||
+      Ld * p.in_stride * 4 > V3_XDEC_BYTES || (c.enc_in & 3))
     return fail(CET_E_INVALID, "v3 LDS layout: staged input or multiplicity table exceeds its region");
   p.lds3_XB = V3L_XB;
   p.lds3_CTX = V3L_CTX;

@@ -107,13 +107,27 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   float* IN = reinterpret_cast<float*>(lds + V3L_CTX);      // staged raw input (aliases CTX)
   float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
 
+  float* XDEC = reinterpret_cast<float*>(lds + V3L_XDEC);   // staged decoder input
+  if (DIAG && a.stamps && threadIdx.x == 0) a.stamps[(size_t)b * MAX_STAMPS + 127] = __builtin_amdgcn_s_memtime();
+  const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride, Ld = PL.dec_len;
+  // this sequence's x_enc and x_dec rows are requested first (one f32x4 per thread each: L·C/4 ≤
+  // 384), so their HBM latency overlaps the LDS zeroing instead of following it
+  const int t4 = 4 * (int)threadIdx.x;
+  f32x4 xe4 = {0.f, 0.f, 0.f, 0.f}, xd4 = xe4;
+  if (t4 < L0 * C) xe4 = *reinterpret_cast<const f32x4*>(a.x_enc + (size_t)b * L0 * C + t4);
+  if (t4 < Ld * C) xd4 = *reinterpret_cast<const f32x4*>(a.x_dec + (size_t)b * Ld * C + t4);
   // zero the activation images: rows past L of Xb / CTX / ENC are read (never used) by MFMAs
   for (int i = threadIdx.x; i < V3L_CNT / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i = V3L_ENC / 16 + (int)threadIdx.x; i < PL.lds3_bytes / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();   // zeroing done before the staged rows land in CTX
+  {
+    const int cm = C - 1;
+    if (t4 < L0 * C) *reinterpret_cast<f32x4*>(IN + (t4 >> PL.C_shift) * CS + (t4 & cm)) = xe4;
+    if (t4 < Ld * C) *reinterpret_cast<f32x4*>(XDEC + (t4 >> PL.C_shift) * CS + (t4 & cm)) = xd4;
+  }
 
-  const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride;
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // bf16x8 per n-tile at K = 128
   Res<MT> X;
   // diagnostics: s_memtime at phase boundaries (wave 0, lane 0), off unless a.stamps is set
@@ -170,9 +184,13 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
 #endif
   };
 
+  auto ESTAMP = [&](int k) {   // embedding sub-phases of encoder 0 (slots 124..126)
+    if (stamps && threadIdx.x == 0) stamps[124 + k] = __builtin_amdgcn_s_memtime();
+  };
   for (int e = 0; e < PL.n_enc; ++e) {
-    stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);
+    if (e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);   // CTX was reused by encoder e-1
     __syncthreads();
+    if (e == 0) ESTAMP(0);
     // ---- DataEmbedding (embed.py:132-135) on the EncoderStack window x[:, -L:] (encoder.py:95-106)
     int L = L0 >> e;
     const int off = L0 - L;
@@ -187,6 +205,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
         X.v[mt] = y + pload4(M, PL.pe_enc, prow * DMODEL + n0);
       });
     }
+    if (e == 0) ESTAMP(1);
     __syncthreads();                       // IN (aliases CTX) fully read
     store_res(X, nmt, L, Xb);
     __syncthreads();
@@ -281,16 +300,14 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
 
   // ================================ decoder (decoder.py:43-56), instantiated for its compile-time
   // tile count (dec_len ≤ 48)
-  const int Ld = PL.dec_len, S = PL.S;
-  stage(a.x_dec + (size_t)b * Ld * C, IN, Ld, C, CS);
-  __syncthreads();
+  const int S = PL.S;
   auto decoder = [&](auto NMDc) __attribute__((always_inline)) {
     constexpr int NMD = decltype(NMDc)::value;
     const int nmd = NMD;
     Res<NMD> XD;
     {
       const GemmDesc d = PL.emb_dec;
-      gemm_res_n<2, NMD>(M, d, LoadEmbedOff{IN, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
+      gemm_res_n<2, NMD>(M, d, LoadEmbedOff{XDEC, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
         const int m = mt * 16 + (lane_op() & 15);
         const int prow = m < LMAX ? m : LMAX - 1;
         XD.v[mt] = y + pload4(M, PL.pe_dec, prow * DMODEL + n0);

@@ -101,14 +101,17 @@ struct InformerPlan {
 // v3 LDS layout, fixed at compile time for every plan (LMAX rows; the kernel folds the offsets into
 // its ds_* immediates and keeps no LDS base in scalar registers): bf16 image | context / FFN hidden /
 // staged input | 8 waves' attention scratch aliased by the LayerNorm partials | multiplicity table |
-// sampler state | encoder-stack output (S rows, the only plan-sized region, last).
+// sampler state | staged decoder input | encoder-stack output (S rows, the only plan-sized
+// region, last).
 constexpr int V3L_XB = 0;
 constexpr int V3L_CTX = V3L_XB + LMAX * BS * 2;
 constexpr int V3L_SCR = V3L_CTX + LMAX * BS * 2;
 constexpr int V3L_CNT = V3L_SCR + (LMAX * LN3_STRIDE * 4 > 8 * V2_SCR_FLOATS * 4 ? LMAX * LN3_STRIDE * 4
                                                                                  : 8 * V2_SCR_FLOATS * 4);
 constexpr int V3L_MT = V3L_CNT + LMAX * 96;
-constexpr int V3L_ENC = V3L_MT + ((624 * 4 + 15) & ~15);
+constexpr int V3L_XDEC = V3L_MT + ((624 * 4 + 15) & ~15);   // staged decoder input, ≤ 48 rows × 20
+constexpr int V3_XDEC_BYTES = 48 * 20 * 4;
+constexpr int V3L_ENC = V3L_XDEC + V3_XDEC_BYTES;
 static_assert(V3L_CTX % 16 == 0 && V3L_SCR % 16 == 0 && V3L_CNT % 16 == 0 && V3L_ENC % 16 == 0, "16-B regions");
 
 // LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded

@@ -63,6 +63,12 @@ def main():
                "barrier", "store_xb+barrier"]
         dd = np.diff(pts, axis=1).mean(axis=0)
         print("L0 fine: " + "  ".join(f"{a} {b:.0f}" for a, b in zip(lab, dd)))
+    e = sub[:, 124:128]
+    if e[:, 0].any():
+        pts = np.stack([e[:, 3], sub[:, 0], e[:, 0], e[:, 1], sub[:, 1]], axis=1)
+        dd = np.diff(pts, axis=1).mean(axis=0)
+        lab = ["entry+LDS zero", "stage x_enc", "embed gemm+pe", "store+barrier"]
+        print("embedding fine: " + "  ".join(f"{a} {b:.0f}" for a, b in zip(lab, dd)))
     for i in range(1, n):
         print(f"{NAMES[i]:22s} mean {d[:, i - 1].mean():9.0f}  p10 {np.percentile(d[:, i - 1], 10):9.0f}  "
               f"p90 {np.percentile(d[:, i - 1], 90):9.0f}  ({100 * d[:, i - 1].mean() / tot.mean():5.1f}%)")
