@@ -9,10 +9,12 @@
 
 namespace cet {
 
+// `plan` is a.plan again as a noalias parameter, so uniform descriptor reads become scalar loads.
 template <int DFF>
-__global__ void __launch_bounds__(NTHREADS, 1) transformer_forward(TransformerArgs a) {
+__global__ void __launch_bounds__(NTHREADS, 1) transformer_forward(TransformerArgs a,
+                                                                   const TransformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const TransformerPlan& pl = *a.plan;
+  const TransformerPlan& pl = *plan;
   const float* __restrict__ P = a.params;
   const bf16x8* __restrict__ W = reinterpret_cast<const bf16x8*>(a.weights);
   const int b = blockIdx.x;
@@ -159,20 +161,20 @@ __global__ void __launch_bounds__(NTHREADS, 1) transformer_forward(TransformerAr
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
   using namespace cet;
   if (a->B <= 0) return 0;
-  auto launch = [&](auto kern) -> int {
-    static bool attr_done = false;
-    if (!attr_done) {
+  static bool attr_done[2] = {false, false};   // one flag per kernel instance
+  auto launch = [&](void (*kern)(TransformerArgs, const TransformerPlan*), int slot) -> int {
+    if (!attr_done[slot]) {
       if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024) != hipSuccess)
         return -1;
-      attr_done = true;
+      attr_done[slot] = true;
     }
-    hipLaunchKernelGGL(kern, dim3(a->B), dim3(NTHREADS), lds_bytes, stream, *a);
+    hipLaunchKernelGGL(kern, dim3(a->B), dim3(NTHREADS), lds_bytes, stream, *a, a->plan);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   };
   switch (dff) {
-    case 64: return launch(transformer_forward<64>);
-    case 128: return launch(transformer_forward<128>);
+    case 64: return launch(transformer_forward<64>, 0);
+    case 128: return launch(transformer_forward<128>, 1);
     default: return -3;
   }
 }

@@ -75,6 +75,7 @@ def time_engine(m, dev, B, steps, warmup=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--only", default="", help="run only the configs whose name contains this")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     runs = [
@@ -85,6 +86,8 @@ def main():
          informer_flops(e_layers=(4, 3), attn="full")),
     ]
     for name, mk, B, flops in runs:
+        if args.only not in name:
+            continue
         m = mk()
         step_ms, kern_ms = time_engine(m, dev, B, args.steps)
         tf = flops * B / (kern_ms * 1e-3) / 1e12
