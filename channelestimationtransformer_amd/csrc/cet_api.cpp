@@ -618,16 +618,21 @@ int build_informer(cet_engine* e) {
   // aliased by the LayerNorm partials | multiplicity table | sampler state (≤ 80 KB: 2 per CU)
   o = 0;
   // (fixed layout, cet_plan.hpp V3L_*: only the stack output's size depends on the plan)
-  if (LMAX * p.in_stride * 4 > V3L_SCR - V3L_CTX || max_cnt > V3L_MT - V3L_CNT || LP > LMAX ||
-      Ld * p.in_stride * 4 > V3_XDEC_BYTES || (c.enc_in & 3))
+  if (LMAX * p.in_stride * 4 > V3L_SCR - V3L_CTX || max_cnt > V3L_MT - V3L_CNT || LP > LMAX || (c.enc_in & 3))
     return fail(CET_E_INVALID, "v3 LDS layout: staged input or multiplicity table exceeds its region");
   p.lds3_XB = V3L_XB;
   p.lds3_CTX = V3L_CTX;
   p.lds3_SCR = V3L_SCR;
   p.lds3_CNT = V3L_CNT;
   p.lds3_MT = V3L_MT;
-  p.lds3_ENC = V3L_ENC;
-  p.lds3_bytes = al(V3L_ENC + SP * BS * 2);
+  if (al(V3L_ENC_XE + SP * BS * 2) <= V3_LDS_2PERCU && Ld * p.in_stride * 4 <= V3_XDEC_BYTES) {
+    p.lds3_XDEC = V3L_XDEC;
+    p.lds3_ENC = V3L_ENC_XE;
+  } else {
+    p.lds3_XDEC = -1;
+    p.lds3_ENC = V3L_ENC;
+  }
+  p.lds3_bytes = al(p.lds3_ENC + SP * BS * 2);
   return CET_OK;
 }
 
@@ -1042,7 +1047,7 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   switch (e->variant) {
     case 1: return cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
     case 2: return cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
-    default: return cet_launch_informer_v3(&a, e->icfg.d_ff, p.lds3_bytes, st);
+    default: return cet_launch_informer_v3(&a, e->icfg.d_ff, p.lds3_bytes, p.lds3_XDEC >= 0, st);
   }
 }
 

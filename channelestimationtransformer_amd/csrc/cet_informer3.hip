@@ -82,7 +82,8 @@ __device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
 
 // DIAG: the instance that honours the optional outputs (attns maps, activation dump, phase stamps);
 // the production instance compiles them out, which frees the scalar registers their pointers held.
-template <int DFF, bool DIAG>
+// XE: the plan's layout has the x_dec region (staged at entry; cet_plan.hpp V3L_XDEC).
+template <int DFF, bool DIAG, bool XE>
 // `plan` is a.plan passed again as a noalias parameter: no store of the kernel can clobber it, so
 // every uniform descriptor read becomes a scalar load (s_load into SGPRs) instead of a vector load
 // plus v_readfirstlane.
@@ -99,7 +100,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
 
   __bf16* Xb = reinterpret_cast<__bf16*>(lds + V3L_XB);
   __bf16* CTX = reinterpret_cast<__bf16*>(lds + V3L_CTX);   // attention context / FFN hidden
-  __bf16* ENC = reinterpret_cast<__bf16*>(lds + V3L_ENC);
+  __bf16* ENC = reinterpret_cast<__bf16*>(lds + (XE ? V3L_ENC_XE : V3L_ENC));
   float* LNP = reinterpret_cast<float*>(lds + V3L_SCR);      // LN partials (alias the scratch)
   uint8_t* CNT = reinterpret_cast<uint8_t*>(lds + V3L_CNT);
   MTState gen{reinterpret_cast<uint32_t*>(lds + V3L_MT), MT_N};
@@ -107,7 +108,8 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   float* IN = reinterpret_cast<float*>(lds + V3L_CTX);      // staged raw input (aliases CTX)
   float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
 
-  float* XDEC = reinterpret_cast<float*>(lds + V3L_XDEC);   // staged decoder input
+  // staged decoder input: its own region (XE, staged at entry) or CTX (staged when the decoder starts)
+  float* XDEC = reinterpret_cast<float*>(lds + (XE ? V3L_XDEC : V3L_CTX));
   if (DIAG && a.stamps && threadIdx.x == 0) a.stamps[(size_t)b * MAX_STAMPS + 127] = __builtin_amdgcn_s_memtime();
   const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride, Ld = PL.dec_len;
   // this sequence's x_enc and x_dec rows are requested first (one f32x4 per thread each: L·C/4 ≤
@@ -115,17 +117,17 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   const int t4 = 4 * (int)threadIdx.x;
   f32x4 xe4 = {0.f, 0.f, 0.f, 0.f}, xd4 = xe4;
   if (t4 < L0 * C) xe4 = *reinterpret_cast<const f32x4*>(a.x_enc + (size_t)b * L0 * C + t4);
-  if (t4 < Ld * C) xd4 = *reinterpret_cast<const f32x4*>(a.x_dec + (size_t)b * Ld * C + t4);
+  if (XE && t4 < Ld * C) xd4 = *reinterpret_cast<const f32x4*>(a.x_dec + (size_t)b * Ld * C + t4);
   // zero the activation images: rows past L of Xb / CTX / ENC are read (never used) by MFMAs
   for (int i = threadIdx.x; i < V3L_CNT / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int i = V3L_ENC / 16 + (int)threadIdx.x; i < PL.lds3_bytes / 16; i += NTHREADS)
+  for (int i = V3L_XDEC / 16 + (int)threadIdx.x; i < PL.lds3_bytes / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();   // zeroing done before the staged rows land in CTX
   {
     const int cm = C - 1;
     if (t4 < L0 * C) *reinterpret_cast<f32x4*>(IN + (t4 >> PL.C_shift) * CS + (t4 & cm)) = xe4;
-    if (t4 < Ld * C) *reinterpret_cast<f32x4*>(XDEC + (t4 >> PL.C_shift) * CS + (t4 & cm)) = xd4;
+    if (XE && t4 < Ld * C) *reinterpret_cast<f32x4*>(XDEC + (t4 >> PL.C_shift) * CS + (t4 & cm)) = xd4;
   }
 
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // bf16x8 per n-tile at K = 128
@@ -301,6 +303,10 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   // ================================ decoder (decoder.py:43-56), instantiated for its compile-time
   // tile count (dec_len ≤ 48)
   const int S = PL.S;
+  if (!XE) {   // no room to keep it since entry: stage it now (into CTX)
+    stage(a.x_dec + (size_t)b * Ld * C, XDEC, Ld, C, CS);
+    __syncthreads();
+  }
   auto decoder = [&](auto NMDc) __attribute__((always_inline)) {
     constexpr int NMD = decltype(NMDc)::value;
     const int nmd = NMD;
@@ -413,10 +419,11 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
 }  // namespace v3
 }  // namespace cet
 
-extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
+extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, int xdec_early,
+                                      hipStream_t stream) {
   using namespace cet;
   if (a->B <= 0) return 0;
-  static bool attr_done[4] = {false, false, false, false};   // one flag per kernel instance
+  static bool attr_done[8] = {};   // one flag per kernel instance
   auto launch = [&](void (*kern)(InformerArgs, const InformerPlan*), int slot) -> int {
     if (!attr_done[slot]) {
       if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -428,11 +435,14 @@ extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int l
     return hipGetLastError() == hipSuccess ? 0 : -2;
   };
   const bool diag = a->attns || a->dbg || a->stamps;
-  switch (dff) {
-    case 64: return diag ? launch(v3::informer_forward_v3<64, true>, 0) : launch(v3::informer_forward_v3<64, false>, 1);
-    case 128: return diag ? launch(v3::informer_forward_v3<128, true>, 2) : launch(v3::informer_forward_v3<128, false>, 3);
-    default: return -3;
-  }
+  const int slot = (dff == 128 ? 4 : 0) + (diag ? 2 : 0) + (xdec_early ? 1 : 0);
+  using K = void (*)(InformerArgs, const InformerPlan*);
+  static const K kerns[8] = {v3::informer_forward_v3<64, false, false>,  v3::informer_forward_v3<64, false, true>,
+                             v3::informer_forward_v3<64, true, false>,   v3::informer_forward_v3<64, true, true>,
+                             v3::informer_forward_v3<128, false, false>, v3::informer_forward_v3<128, false, true>,
+                             v3::informer_forward_v3<128, true, false>,  v3::informer_forward_v3<128, true, true>};
+  if (dff != 64 && dff != 128) return -3;
+  return launch(kerns[slot], slot);
 }
 
 namespace cet {

@@ -71,7 +71,8 @@ extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_
 extern "C" int cet_launch_informer_v2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
                                        uint8_t* tab_out, int lds_bytes, hipStream_t stream);
-extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, int xdec_early,
+                                      hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);

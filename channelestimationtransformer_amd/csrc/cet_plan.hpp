@@ -93,6 +93,7 @@ struct InformerPlan {
   int lds2_XB, lds2_CTX, lds2_ENC, lds2_LN, lds2_SCR, lds2_CNT, lds2_MT, lds2_bytes;
   // v3 (8-wave) layout: the LayerNorm partials alias the per-wave attention scratch
   int lds3_XB, lds3_CTX, lds3_ENC, lds3_SCR, lds3_CNT, lds3_MT, lds3_bytes;
+  int lds3_XDEC;            // staged decoder input (byte offset), or -1
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
   int draws;                // mt19937 words one forward consumes (Σ LQ·U over every call)
@@ -101,7 +102,7 @@ struct InformerPlan {
 // v3 LDS layout, fixed at compile time for every plan (LMAX rows; the kernel folds the offsets into
 // its ds_* immediates and keeps no LDS base in scalar registers): bf16 image | context / FFN hidden /
 // staged input | 8 waves' attention scratch aliased by the LayerNorm partials | multiplicity table |
-// sampler state | staged decoder input | encoder-stack output (S rows, the only plan-sized
+// sampler state | [staged decoder input] | encoder-stack output (S rows, the only plan-sized
 // region, last).
 constexpr int V3L_XB = 0;
 constexpr int V3L_CTX = V3L_XB + LMAX * BS * 2;
@@ -111,8 +112,13 @@ constexpr int V3L_CNT = V3L_SCR + (LMAX * LN3_STRIDE * 4 > 8 * V2_SCR_FLOATS * 4
 constexpr int V3L_MT = V3L_CNT + LMAX * 96;
 constexpr int V3L_XDEC = V3L_MT + ((624 * 4 + 15) & ~15);   // staged decoder input, ≤ 48 rows × 20
 constexpr int V3_XDEC_BYTES = 48 * 20 * 4;
-constexpr int V3L_ENC = V3L_XDEC + V3_XDEC_BYTES;
-static_assert(V3L_CTX % 16 == 0 && V3L_SCR % 16 == 0 && V3L_CNT % 16 == 0 && V3L_ENC % 16 == 0, "16-B regions");
+constexpr int V3L_ENC_XE = V3L_XDEC + V3_XDEC_BYTES;   // stack output after the staged decoder input
+constexpr int V3L_ENC = V3L_XDEC;                      // ... or in its place (decoder input staged late)
+constexpr int V3_LDS_2PERCU = 80 * 1024;               // two sequences per CU
+// The kernel instance with the x_dec region (XE) is used when the plan still fits two workgroups
+// per CU with it (InformerPlan::lds3_XDEC = V3L_XDEC), else x_dec is staged into CTX when the
+// decoder starts (lds3_XDEC = -1).
+static_assert(V3L_CTX % 16 == 0 && V3L_SCR % 16 == 0 && V3L_CNT % 16 == 0 && V3L_ENC_XE % 16 == 0, "16-B regions");
 
 // LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded
 // mt19937 state | the forward's tempered words | every call's multiplicity table.
