@@ -53,14 +53,26 @@ __global__ void __launch_bounds__(1024) nmse_split_rows(const float* __restrict_
   if (g < nb) {
     const f32x4* P = reinterpret_cast<const f32x4*>(pred);
     const f32x4* X = reinterpret_cast<const f32x4*>(label);
-    for (int b = g; b < B; b += nb) {
-      const f32x4 xh = __builtin_nontemporal_load(P + (size_t)b * R4 + j);
-      const f32x4 x = __builtin_nontemporal_load(X + (size_t)b * R4 + j);
+    // batches of KB sequences: all 2·KB loads are issued before the first fma, so the loop pays one
+    // memory latency per batch instead of one per sequence; the fp64 sums keep the sequential order
+    constexpr int KB = 12;
+    for (int b0 = g; b0 < B; b0 += KB * nb) {
+      f32x4 xh[KB], x[KB];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double d = (double)x[r] - (double)xh[r];
-        mse = fma(d, d, mse);
-        pw = fma((double)xh[r], (double)xh[r], pw);
+      for (int k = 0; k < KB; ++k) {
+        const int b = b0 + k * nb;
+        xh[k] = b < B ? P[(size_t)b * R4 + j] : f32x4{0.f, 0.f, 0.f, 0.f};
+        x[k] = b < B ? X[(size_t)b * R4 + j] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        if (b0 + k * nb >= B) break;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double d = (double)x[k][r] - (double)xh[k][r];
+          mse = fma(d, d, mse);
+          pw = fma((double)xh[k][r], (double)xh[k][r], pw);
+        }
       }
     }
   }
