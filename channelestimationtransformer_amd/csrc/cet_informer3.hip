@@ -307,7 +307,9 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
     stage(a.x_dec + (size_t)b * Ld * C, XDEC, Ld, C, CS);
     __syncthreads();
   }
-  auto decoder = [&](auto NMDc) __attribute__((always_inline)) {
+  // NMSc: compile-time bound on the cross-attention key tiles (the encoder-stack output rows)
+  auto decoder = [&](auto NMDc, auto NMSc) __attribute__((always_inline)) {
+    constexpr int NMS = decltype(NMSc)::value;
     constexpr int NMD = decltype(NMDc)::value;
     const int nmd = NMD;
     Res<NMD> XD;
@@ -341,7 +343,7 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
       {
         // cross-attention: FullAttention over the encoder-stack output, mix=False
         const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
-        attend(IC<NMD>{}, IC<MT>{}, Xb, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+        attend(IC<NMD>{}, IC<NMS>{}, Xb, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
                part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
       }
       const WPre<4> pco = prefetch_res<4>(M, DLD.co);
@@ -387,9 +389,9 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
   };
 #ifndef V3_NO_DEC
   switch ((Ld + 15) >> 4) {
-    case 1: decoder(IC<1>{}); break;
-    case 2: decoder(IC<2>{}); break;
-    default: decoder(IC<3>{}); break;
+    case 1: S <= 16 ? decoder(IC<1>{}, IC<1>{}) : decoder(IC<1>{}, IC<MT>{}); break;
+    case 2: S <= 16 ? decoder(IC<2>{}, IC<1>{}) : decoder(IC<2>{}, IC<MT>{}); break;
+    default: S <= 16 ? decoder(IC<3>{}, IC<1>{}) : decoder(IC<3>{}, IC<MT>{}); break;
   }
 #endif
   // ---- the first workgroup to finish prepares the NEXT forward's ProbSparse tables from the
