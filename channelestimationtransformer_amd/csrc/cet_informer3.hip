@@ -221,9 +221,18 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
       // ---- AttentionLayer + ProbAttention / FullAttention, one head per wave, context → CTX
       {
         const GemmDesc q = ELD.qkv;
-        attend(IC<MT>{}, IC<MT>{}, Xb, Xb, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
-               part_of(q, 0), part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
-               DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
+        // instantiated for the layer's compile-time tile bound (distilled layers: 3, 2, 1 tiles)
+        auto enc_attend = [&](auto NQ) __attribute__((always_inline)) {
+          attend(NQ, NQ, Xb, Xb, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
+                 part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
+                 DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
+        };
+        switch (nmt) {
+          case 1: enc_attend(IC<1>{}); break;
+          case 2: enc_attend(IC<2>{}); break;
+          case 3: enc_attend(IC<3>{}); break;
+          default: enc_attend(IC<MT>{}); break;
+        }
       }
       const WPre<4> po = prefetch_res<4>(M, ELD.o);   // x = x + new_x (encoder.py:49)
       __syncthreads();
