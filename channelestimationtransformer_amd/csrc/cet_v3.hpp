@@ -466,8 +466,9 @@ __device__ __forceinline__ void attention_head(const HeadIO& io, const Mem& m, i
   if (sparse) {
     // ---- sparsity measurement M (attn.py:95-105) from key multiplicities (LDS-staged table)
     const float invLK = 1.0f / (float)LK;
-#pragma unroll 1
-    for (int qt = 0; qt < nqt; ++qt) {
+#pragma unroll
+    for (int qt = 0; qt < MQ; ++qt) {
+      if (qt >= nqt) break;
       const int q = qt * 16 + col;
       const bf16x4 qf = project_q(q);
       // this lane's six count words (keys 16kt + 4g + r, kt = 0..5) are contiguous: cnt_pos_v2()
