@@ -359,12 +359,12 @@ __global__ void __launch_bounds__(NTHREADS, 4) informer_forward_v3(InformerArgs 
       __syncthreads();
       STAMP();  // cross-attention
       gemm_res_n<4, NMD>(pco, LoadBF16{CTX}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      const WPre<4> pf1 = prefetch_tiles<4>(M, DLD.f1, DFF / 16);
       ln_res(XD, nmd, Ld, M, DLD.ln2, 1e-5f, false, LNP, Xb);
       __syncthreads();
       {
-        const GemmDesc d = DLD.f1;
         const int relu = PL.act_relu;
-        gemm_tiles<4>(M, d, DFF / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
+        gemm_tiles1<4>(pf1, DFF / 16, nmd, LoadBF16{Xb}, [&](int mt, int n0, f32x4 v) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
           *reinterpret_cast<bf16x4*>(CTX + (mt * 16 + (lane_op() & 15)) * BS + n0) = cvt4(v);
