@@ -96,16 +96,24 @@ __global__ void __launch_bounds__(1024) nmse_split_rows(const float* __restrict_
     part[1][threadIdx.x] = p1;
   }
   __syncthreads();
-  if ((int)threadIdx.x < T) {
-    const int t = threadIdx.x;
+  // stage 2: wave w folds step t = w (+16…): lanes stride the nb group partials, then a fixed
+  // xor-butterfly — a fixed order (deterministic) without a serial nb-long LDS chain
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int t = wave; t < T; t += 16) {
     double a = 0.0, p = 0.0;
-    for (int gg = 0; gg < nb; ++gg) {
+    for (int gg = lane; gg < nb; gg += 64) {
       a += part[0][t * nb + gg];
       p += part[1][t * nb + gg];
     }
-    const float r = (float)(a / p);
-    out[t] = accumulate ? out[t] + r : r;
-    if (last) last[t] = r;
+    for (int m = 32; m >= 1; m >>= 1) {
+      a += __shfl_xor(a, m, 64);
+      p += __shfl_xor(p, m, 64);
+    }
+    if (lane == 0) {
+      const float r = (float)(a / p);
+      out[t] = accumulate ? out[t] + r : r;
+      if (last) last[t] = r;
+    }
   }
 }
 
