@@ -3,14 +3,17 @@
 A step = one inference forward of a batch of ``--batch`` (default 512) independent channel
 sequences (x_enc [90,16], x_dec [15,16] → out [5,16]) through the fused HIP kernel, with a
 fresh torch-compatible ProbSparse index draw (native mt19937, as torch.randint would), plus
-the NMSE_Split reduction of that batch accumulated on device (run_validation's
+the NMSE_Split reduction of that batch on the device (run_validation's
 ``loss += NMSELossSplit(output, label)``, QuantizationAwareTraining.py:115-122).
 Inputs are synthetic channels resident in HBM; weights are the seeded synthetic recipe.
 
-Multi-GPU (launched by torch.distributed.run): one process per GPU, each with its own
-512-sequence shard (weak scaling, no collective in the data path); after the timed loop the
-per-rank NMSE accumulators are all-reduced and the last step's predictions all-gathered over
-RCCL for the NMSE reduction.  Rank 0 prints ONE JSON line.
+Multi-GPU: ``python bench.py --gpus N`` starts N rank processes itself (torch.distributed.run in a
+child process, before anything touches the GPU); the driver may also launch it under torchrun.
+One process per GPU, each with its own 512-sequence shard of an N×512 global batch (weak scaling,
+no collective in the data path).  Every rank keeps the raw fp64 NMSE_Split sums of its shard per
+step; after the timed loop one all_reduce gives each step's ratio over the whole global batch, and
+one all_gather collates the last step's predictions on rank 0, which reduces NMSE_Split over them
+itself and checks it against the all-reduced sums.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -26,12 +29,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
-KERNEL_NAMES = {1: "cet::informer_forward<64>", 2: "cet::v2::informer_forward_v2<64>",
+KERNEL_NAMES = {1: "cet::informer_forward<64>",
                 3: "cet::v3::informer_forward_v3<64, false, true>"}
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
            n_heads=8, e_layers=[4], d_layers=3, d_ff=64, dropout=0.05, attn="prob", embed="fixed",
            activation="gelu", output_attention=False, distil=True)
+WORKLOAD = ("FullPrecision InformerStack inference (C2): ProbSparse attn, distil, e_layers=[4], d_layers=3, "
+            "d_model=128, n_heads=8, d_ff=64, seq_len=90, label_len=10, pred_len=5")
 
 
 def build_model(device):
@@ -51,72 +56,154 @@ def build_model(device):
     return m.eval()
 
 
-def cpu_baseline(seconds: float = 12.0, batch: int = 32):
-    """The numpy oracle (a restatement of the reference CPU forward, float32) on host cores."""
+def cpu_baseline(batch: int = 512, reps: int = 5):
+    """The reference's own PyTorch CPU forward (oracle/informer_torch.py: the aten ops of
+    FullPrecision/InformerModel in eval/no_grad, float32) on this host's cores: median of ``reps``
+    forwards at B=512 (the GPU workload) and of 20 at B=1."""
+    import torch
+
     from channelestimationtransformer_amd.dataset import make_batch
     from channelestimationtransformer_amd.rng import draw_indices
     from channelestimationtransformer_amd.spec import informer_stack_spec
     from channelestimationtransformer_amd.weights import synthetic_state_dict
-    from oracle.informer_np import InformerConfig, InformerOracle, sample_shapes
+    from oracle.informer_np import InformerConfig, sample_shapes
+    from oracle.informer_torch import TorchInformer, host_cpu
 
-    cfg = InformerConfig()
-    orc = InformerOracle(cfg, synthetic_state_dict(informer_stack_spec(16, 16, 16, 128, 8, [4], 3, 64, freq="gelu"), 0),
-                         dtype=np.float32)
-    xe, xd, _ = make_batch(batch, seed=99)
-    shapes = sample_shapes(cfg)
-    orc.forward(xe, xd, draw_indices(shapes, seed=0))   # warm-up
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        orc.forward(xe, xd, draw_indices(shapes, seed=n))
-        n += 1
-    dt = time.perf_counter() - t0
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": round(n * batch / dt, 2), "unit": "seq/s", "cores": threads, "kind": "port",
-            "sample": f"{n} forwards of B={batch} (numpy oracle, float32, {dt:.1f}s)"}
+    host = host_cpu()
+    threads = min(v for v in (host["physical_cores"], host["usable_logical"],
+                              int(os.environ.get("OMP_NUM_THREADS", "0")) or None) if v)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        cfg = InformerConfig()
+        model = TorchInformer(cfg, synthetic_state_dict(informer_stack_spec(16, 16, 16, 128, 8, [4], 3, 64,
+                                                                            freq="gelu"), 0), dtype=torch.float32)
+        shapes = sample_shapes(cfg)
+
+        def med(b, n, warm):
+            xe, xd, _ = make_batch(b, seed=99)
+            xe, xd = torch.from_numpy(xe), torch.from_numpy(xd)
+            ts = []
+            for i in range(warm + n):
+                idx = draw_indices(shapes, seed=i)
+                t0 = time.perf_counter()
+                model.forward(xe, xd, idx)
+                if i >= warm:
+                    ts.append(time.perf_counter() - t0)
+            return float(np.median(ts))
+
+        t_big = med(batch, reps, 1)
+        t_one = med(1, 20, 3)
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(batch / t_big, 1), "unit": "seq/s", "cores": threads, "kind": "port",
+            "sample": f"median of {reps} forwards at B={batch} ({t_big * 1e3:.0f} ms each) of the reference's torch "
+                      f"CPU forward (oracle/informer_torch.py, float32, eval/no_grad, {threads} threads)",
+            "b1_seq_per_s": round(1.0 / t_one, 1), "cpu_model": host["model"],
+            "host_physical_cores": host["physical_cores"], "host_usable_logical": host["usable_logical"]}
 
 
 def load_traffic(profile_dir, kernel):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary (None if the summary
-    was collected on another kernel variant)."""
+    was collected on another kernel variant), and the file it came from."""
     path = os.path.join(profile_dir, "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
             d = json.load(f)
         if kernel not in (d.get("kernel") or ""):
-            return None
-        return d.get("hbm_bytes_per_launch")
+            return None, None
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--settle-s", type=float, default=1.0,
+                    help="keep warming up (untimed) until this many seconds have passed, so the GPU clock has "
+                         "settled even with a short --warmup")
     ap.add_argument("--batch", type=int, default=512, help="sequences per GPU per step")
     ap.add_argument("--snr", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--variant", type=int, default=3,
-                    help="fused-kernel generation (1: LDS-resident, 2: 4-wave register-resident, 3: 8-wave)")
+                    help="fused-kernel generation (1: LDS-resident, 3: 8-wave register-resident)")
     ap.add_argument("--sampler", choices=("device", "host"), default="device",
                     help="where the native ProbSparse draws run (identical streams; DESIGN §3.3)")
-    ap.add_argument("--nmse-stream", choices=("same", "side"), default="same",
-                    help="side: NMSE_Split of step n runs on a second stream, overlapping forward n+1 "
-                         "(predictions double-buffered)")
-    args = ap.parse_args()
+    ap.add_argument("--collation-selftest", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank spawn and NMSE collation (no GPU, no engine)")
+    return ap.parse_args(argv)
 
+
+def collate_and_report(sums, out_last, lab, world, rank, nmse_fn):
+    """After the timed loop: all_reduce the per-step sums, all_gather the last predictions on rank 0
+    and check NMSE_Split over them against the all-reduced sums of the same step."""
     import torch
 
+    from channelestimationtransformer_amd.sharding import check_gathered_nmse, collate_step_sums, gather_predictions
+
+    ratios, nmse = collate_step_sums(sums, world)
+    preds = gather_predictions(out_last, world)
+    labels = gather_predictions(lab, world)
+    check = None
+    if rank == 0:
+        g = nmse_fn(torch.cat(preds).contiguous(), torch.cat(labels).contiguous())
+        check = check_gathered_nmse(g, ratios[-1])
+    return nmse.cpu().numpy(), check
+
+
+def selftest(args, world, rank):
+    """--collation-selftest: the multi-rank launch and the exact collation code of the GPU run, on CPU
+    with gloo and seeded stand-in predictions (no kernel runs; nothing is timed)."""
+    import torch
+    import torch.distributed as dist
+
+    from channelestimationtransformer_amd.sharding import nmse_split_torch
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(1234 + 7919 * rank)
+    T = CFG["pred_len"]
+    lab = torch.randn(args.batch, T, 16, generator=g)
+    sums = torch.zeros(args.steps, 2, T, dtype=torch.float64)
+    out = None
+    for s in range(args.steps):
+        out = lab + 0.1 * (s + 1) * torch.randn(args.batch, T, 16, generator=g)
+        p = out.double()
+        d = lab.double() - p
+        sums[s, 0], sums[s, 1] = (d * d).sum((0, 2)), (p * p).sum((0, 2))
+    nmse, check = collate_and_report(sums, out, lab, world, rank, nmse_split_torch)
+    if rank == 0:
+        print(json.dumps({"selftest": "collation", "world": world, "backend": "gloo" if world > 1 else None,
+                          "steps": args.steps, "global_batch": args.batch * world,
+                          "nmse": [float(v) for v in nmse], "gathered_vs_allreduced_rel": check}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # start the N ranks ourselves: a fresh process per GPU; nothing here has touched the GPU
+        from channelestimationtransformer_amd.sharding import spawn_ranks
+
+        rest = list(argv) if argv is not None else sys.argv[1:]
+        raise SystemExit(spawn_ranks(args.gpus, [os.path.abspath(__file__)] + rest))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus > 1 and world != args.gpus:
-        raise SystemExit("for --gpus N>1 launch with: python -m torch.distributed.run --nproc-per-node N "
-                         "--master-addr 127.0.0.1 bench.py --gpus N")
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.collation_selftest:
+        return selftest(args, world, rank)
+
+    import torch
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -126,7 +213,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from channelestimationtransformer_amd.dataset import make_batch
-    from channelestimationtransformer_amd.engine import nmse_split
+    from channelestimationtransformer_amd.engine import nmse_split, nmse_split_sums
     from channelestimationtransformer_amd.flops import informer_flops, io_bytes
 
     model = build_model(dev)
@@ -134,62 +221,51 @@ def main():
     eng.set_variant(args.variant)
     eng.set_sampler(args.sampler == "host")
     eng.seed(1)                 # every rank draws the same index samples (shared across the batch)
-    B = args.batch
+    B, T = args.batch, CFG["pred_len"]
     xe_np, xd_np, lab_np = make_batch(B, snr=args.snr, seed=1234 + 7919 * rank)
     xe = torch.from_numpy(xe_np).to(dev)
     xd = torch.from_numpy(xd_np).to(dev)
     lab = torch.from_numpy(lab_np).to(dev)
-    outs = [torch.empty(B, 5, 16, device=dev) for _ in range(2)]
-    acc = torch.zeros(5, device=dev)
-    main_s = torch.cuda.current_stream(dev)
-    stream = main_s.cuda_stream
-    side_s = torch.cuda.Stream(dev) if args.nmse_stream == "side" else None
-    fwd_done = torch.cuda.Event()
-    nmse_done = [torch.cuda.Event(), torch.cuda.Event()]
-    n_step = [0]
+    out = torch.empty(B, T, 16, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    warm_sums = torch.zeros(2, T, dtype=torch.float64, device=dev)
+    sums = torch.zeros(args.steps, 2, T, dtype=torch.float64, device=dev)
 
-    def step():
-        if side_s is None:
-            eng.forward(xe, xd, outs[0], None, stream)
-            nmse_split(outs[0], lab, acc, accumulate=True, stream=stream)
-            return
-        i = n_step[0] & 1
-        n_step[0] += 1
-        main_s.wait_event(nmse_done[i])       # NMSE of step n-2 has finished reading outs[i]
-        eng.forward(xe, xd, outs[i], None, stream)
-        fwd_done.record(main_s)
-        side_s.wait_event(fwd_done)
-        nmse_split(outs[i], lab, acc, accumulate=True, stream=side_s.cuda_stream)
-        nmse_done[i].record(side_s)
+    def step(k):
+        eng.forward(xe, xd, out, None, stream)
+        nmse_split_sums(out, lab, sums[k] if k >= 0 else warm_sums, stream=stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    acc.zero_()
+    t_w = time.perf_counter()
+    n_warm = 0
+    while n_warm < args.warmup or time.perf_counter() - t_w < args.settle_s:
+        for _ in range(64 if n_warm >= args.warmup else 1):
+            step(-1)
+            n_warm += 1
+        if n_warm >= args.warmup:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     eng.timing(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
+    dt_rank = time.perf_counter() - t0
     kern_ms, launches = eng.timing_read()
     eng.timing(False)
-    from channelestimationtransformer_amd.sharding import collate_nmse, gather_predictions
 
-    dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    per_rank = [dt_rank]
     if dist:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
-    nmse = collate_nmse(acc, args.steps, world).cpu().numpy()     # RCCL all_reduce of NMSE partials
-    out = outs[(n_step[0] - 1) & 1] if side_s is not None else outs[0]
-    gather_predictions(out, world)                                # RCCL all_gather of the last predictions
+        allt = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(allt, torch.tensor([dt_rank], dtype=torch.float64, device=dev))
+        per_rank = [float(t.item()) for t in allt]
+    dt = max(per_rank)
+    nmse, check = collate_and_report(sums, out, lab, world, rank, lambda p, y: nmse_split(p, y))
 
     if rank == 0:
         flops = informer_flops()
@@ -215,6 +291,7 @@ def main():
             parity = float(np.sum((a - r) ** 2) / np.sum(r ** 2))
         except Exception as exc:  # pragma: no cover - reported, not fatal
             parity = f"error: {exc}"
+        traffic, traffic_src = load_traffic(os.path.join(ROOT, "profiles"), KERNEL_NAMES[args.variant])
         res = {
             "metric": METRIC,
             "value": round(seqs / dt, 1),
@@ -228,22 +305,24 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (seeded Jakes channels, SNR %g dB; seeded synthetic weights)" % args.snr,
-            "config": {"workload": "FullPrecision InformerStack inference (C2): ProbSparse attn, distil, "
-                                   "e_layers=[4], d_layers=3, d_model=128, n_heads=8, d_ff=64, seq_len=90, "
-                                   "label_len=10, pred_len=5",
-                       "batch_per_gpu": B, "global_batch": B * world, "parallelism": f"dp{world}",
-                       "nmse_stream": args.nmse_stream},
+            "config": {"workload": WORKLOAD, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"dp{world}"},
+            "world": world,
+            "backend": "nccl" if world > 1 else None,
+            "per_rank_ms_per_step": [round(t / args.steps * 1e3, 4) for t in per_rank],
+            "warmup_steps_run": n_warm,
             "nmse_db": [round(float(10 * np.log10(v)), 3) for v in nmse],
+            "nmse_gathered_vs_allreduced_rel": check,
             "parity_rel_nmse_vs_oracle": parity,
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
-                         "traffic": load_traffic(os.path.join(ROOT, "profiles"), KERNEL_NAMES[args.variant]),
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": KERNEL_NAMES[args.variant], "kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(B)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()

@@ -9,6 +9,8 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -18,6 +20,18 @@
 #include "cet_plan.hpp"
 
 using namespace cet;
+
+bool cet::ensure_lds_attr(const void* kern) {
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({dev, kern})) return true;
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return false;
+  done.insert({dev, kern});
+  return true;
+}
 
 namespace {
 
@@ -93,7 +107,7 @@ struct cet_engine {
   std::vector<std::string> order;
   bool dirty = true;
   bool uploaded = false;
-  int variant = 3;   // fused-kernel generation (CET_KERNEL=v1 / v2 select the older kernels)
+  int variant = 3;   // fused-kernel generation (CET_KERNEL=v1 selects the LDS-resident kernel)
 
   // packed blobs
   std::vector<uint16_t> wblob;
@@ -347,14 +361,19 @@ struct Packer {
 };
 
 // LSQ weight grid (LSQ.py:65-74): q = round_half_even(clamp(w/s, Qn, Qp)); w_q = q·s.  The
-// integer q (exact in bf16 for |q| ≤ 256) is packed and s is applied in the epilogue.
-void lsq_grid(std::vector<float>& w, float s, int bits) {
+// integer q is packed and s is applied in the epilogue; q is exact in bf16 while |q| ≤ 256, which
+// the LSQ initialisation s = mean|w|/√Qp keeps for every width up to 16 bits (|q| ≲ 2·√Qp).  Returns
+// max |q| so the packer can refuse a grid bf16 cannot hold.
+float lsq_grid(std::vector<float>& w, float s, int bits) {
   const float qn = -(float)(1 << (bits - 1)), qp = (float)((1 << (bits - 1)) - 1);
+  float qmax = 0.f;
   for (auto& x : w) {
     float v = x / s;
     v = v < qn ? qn : (v > qp ? qp : v);
     x = std::nearbyint(v);
+    qmax = std::max(qmax, std::fabs(x));
   }
+  return qmax;
 }
 
 int build_informer(cet_engine* e) {
@@ -369,6 +388,7 @@ int build_informer(cet_engine* e) {
   std::memset(&p, 0, sizeof(p));
   const bool lsq = c.lsq_bits > 0;
   const int bits = c.lsq_bits;
+  float qmax = 0.f;   // largest |q| of the LSQ integer grids
 
   auto lin = [&](const std::string& n) { return e->W(n + ".weight"); };
   // Linear/conv1x1 (possibly several concatenated along the output axis) → GemmDesc
@@ -380,7 +400,7 @@ int build_informer(cet_engine* e) {
       float step = 1.f;
       if (lsq && e->has(n + ".step_size")) {
         step = e->scalar(n + ".step_size");
-        lsq_grid(wi, step, bits);
+        qmax = std::max(qmax, lsq_grid(wi, step, bits));
       }
       w.insert(w.end(), wi.begin(), wi.end());
       const auto& bi = e->W(n + ".bias");
@@ -482,7 +502,7 @@ int build_informer(cet_engine* e) {
         float step = 1.f;
         if (lsq && e->has(cp + ".downConv.step_size")) {
           step = e->scalar(cp + ".downConv.step_size");
-          lsq_grid(w, step, bits);
+          qmax = std::max(qmax, lsq_grid(w, step, bits));
         }
         std::vector<float> m((size_t)D * 3 * D);
         for (int n = 0; n < D; ++n)
@@ -519,6 +539,9 @@ int build_informer(cet_engine* e) {
     dbg += (int64_t)L * D;
   }
   p.S = S;
+  if (qmax > 256.f)
+    return fail(CET_E_INVALID, "LSQ grid with |q| = " + std::to_string((int)qmax) +
+                                   " > 256 is not exact in bf16 (step sizes too small for the bit width)");
   const int Ld = c.label_len + c.out_len;
   p.dbg_dec_emb = (int)dbg;
   jstage("dec_emb", dbg, Ld, D);
@@ -664,7 +687,7 @@ int check_informer_config(const cet_informer_config& c) {
   if (c.d_layers < 1 || c.d_layers > MAX_DEC_LAYERS) return fail(CET_E_INVALID, "1..8 decoder layers");
   if (c.c_out < 1 || c.c_out > 128) return fail(CET_E_INVALID, "c_out must be in [1, 128]");
   if (c.factor < 1) return fail(CET_E_INVALID, "factor must be >= 1");
-  if (c.lsq_bits < 0 || c.lsq_bits > 9) return fail(CET_E_INVALID, "lsq_bits must be 0 or 2..9");
+  if (c.lsq_bits < 0 || c.lsq_bits == 1 || c.lsq_bits > 16) return fail(CET_E_INVALID, "lsq_bits must be 0 or 2..16");
   return CET_OK;
 }
 
@@ -707,6 +730,10 @@ int upload(cet_engine* e) {
       if (t) HIP_TRY(hipFree(t));
       HIP_TRY(hipMalloc((void**)&t, e->cnt_bytes));
     }
+    // Prepared tables pending: d_mt[mt_cur] is already past their draws, which no forward has
+    // consumed yet.  Dropping them means the next forward must restart from the host mirror
+    // (the state after the forwards actually launched), not from d_mt[mt_cur].
+    if (e->tab_ready) e->dev_mt_valid = false;
     e->tab_ready = false;
     e->draws_per_forward = 0;
     for (const auto& c : e->calls) e->draws_per_forward += (int64_t)c.LQ * c.U;
@@ -886,7 +913,7 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   e->kind = 0;
   e->icfg = *cfg;
   if (const char* v = std::getenv("CET_KERNEL"))
-    e->variant = std::strcmp(v, "v1") == 0 ? 1 : (std::strcmp(v, "v2") == 0 ? 2 : 3);
+    e->variant = std::strcmp(v, "v1") == 0 ? 1 : 3;
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
   const auto& c = *cfg;
@@ -973,8 +1000,7 @@ int cet_set_prob_indices(cet_engine* e, int call, const int32_t* idx, int L_Q, i
   for (int i = 0; i < L_Q * U; ++i)
     if (idx[i] < 0 || idx[i] >= c.LK) return fail(CET_E_INVALID, "index out of range");
   e->idx[call].assign(idx, idx + (size_t)L_Q * U);
-  e->idx_set[call] = true;
-  e->native_rng = false;
+  e->idx_set[call] = true;   // one-shot: consumed by the next forward; a seeded native stream is not touched
   return CET_OK;
 }
 
@@ -999,6 +1025,21 @@ int64_t cet_native_draw(cet_engine* e, int32_t* out, int64_t n_max) {
   int64_t k = 0;
   for (const auto& c : e->calls)
     for (int i = 0; i < c.LQ * c.U; ++i) out[k++] = (int32_t)(e->rng.next() % (uint32_t)c.LK);
+  return n;
+}
+
+int64_t cet_peek_draw(cet_engine* e, int32_t* out, int64_t n_max) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (!e->native_rng) return fail(CET_E_STATE, "call cet_seed first");
+  int64_t n = 0;
+  for (const auto& c : e->calls) n += (int64_t)c.LQ * c.U;
+  if (!out) return n;
+  if (n_max < n) return fail(CET_E_INVALID, "buffer too small");
+  e->sync_host_rng();        // the host mirror catches up with the launched forwards (device copy unaffected)
+  MT19937 r = e->rng;        // draw from a copy: the stream does not move
+  int64_t k = 0;
+  for (const auto& c : e->calls)
+    for (int i = 0; i < c.LQ * c.U; ++i) out[k++] = (int32_t)(r.next() % (uint32_t)c.LK);
   return n;
 }
 
@@ -1046,7 +1087,6 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   const InformerPlan& p = e->ip;
   switch (e->variant) {
     case 1: return cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
-    case 2: return cet_launch_informer_v2(&a, e->icfg.d_ff, p.lds2_bytes, st);
     default: return cet_launch_informer_v3(&a, e->icfg.d_ff, p.lds3_bytes, p.lds3_XDEC >= 0, st);
   }
 }
@@ -1092,7 +1132,16 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.dbg = e->dbg;
   a.stamps = e->stamps;
   a.B = B;
-  if (e->variant >= 2 && e->native_rng && p.n_calls && !e->host_sampler) {
+  // explicit indices (cet_set_prob_indices for every call) win for this one forward
+  bool explicit_idx = p.n_calls > 0, any_idx = false;
+  for (int c = 0; c < p.n_calls; ++c) {
+    explicit_idx = explicit_idx && e->idx_set[c];
+    any_idx = any_idx || e->idx_set[c];
+  }
+  if (any_idx && !explicit_idx) return fail(CET_E_STATE, "ProbSparse indices set for some calls only");
+  if (p.n_calls && !explicit_idx && !e->native_rng)
+    return fail(CET_E_STATE, "ProbSparse indices not set (cet_set_prob_indices for every call, or cet_seed)");
+  if (e->variant >= 3 && e->native_rng && p.n_calls && !e->host_sampler && !explicit_idx) {
     // ---- resident sampler: the kernel replays this forward's draws itself (cet_mt.hpp)
     if (!e->dev_mt_valid) {
       e->sync_host_rng();
@@ -1142,7 +1191,8 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     return CET_OK;
   }
   // ---- this forward's ProbSparse draws → key multiplicity tables (host-built)
-  if (e->native_rng) {
+  const bool native_now = e->native_rng && !explicit_idx;
+  if (native_now) {
     e->sync_host_rng();
     e->dev_mt_valid = false;
   }
@@ -1150,21 +1200,20 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   e->slot = (e->slot + 1) % cet_engine::NSLOT;
   if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
   uint8_t* h = e->h_cnt[k];
-  const bool v2 = e->variant >= 2;   // v2 and v3 share the count-row layout
+  const bool v2 = e->variant >= 3;   // v3 count-row layout (cnt_pos_v2)
   if (p.n_calls) {
     std::memset(h, 0, e->cnt_bytes);
     for (int c = 0; c < p.n_calls; ++c) {
       const auto& sh = e->calls[c];
       const AttnCall& ac = p.calls[c];
       uint8_t* tab = h + ac.cnt_off;
-      if (e->native_rng) {
+      if (native_now) {
         for (int q = 0; q < sh.LQ; ++q)
           for (int j = 0; j < sh.U; ++j) {
             const int key = (int)(e->rng.next() % (uint32_t)sh.LK);
             tab[q * ac.cnt_stride + (v2 ? cnt_pos_v2(key) : key)]++;
           }
       } else {
-        if (!e->idx_set[c]) return fail(CET_E_STATE, "ProbSparse indices not set for call " + std::to_string(c));
         const int32_t* id = e->idx[c].data();
         for (int q = 0; q < sh.LQ; ++q)
           for (int j = 0; j < sh.U; ++j) {
@@ -1173,7 +1222,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
           }
       }
     }
-    if (!e->native_rng) e->idx_set.assign(e->calls.size(), false);
+    if (explicit_idx) e->idx_set.assign(e->calls.size(), false);
     HIP_TRY(hipMemcpyAsync(e->d_cnt[k], h, e->cnt_bytes, hipMemcpyHostToDevice, st));
     HIP_TRY(hipEventRecord(e->ev[k], st));
     e->ev_used[k] = true;
@@ -1201,7 +1250,7 @@ int cet_set_sampler(cet_engine* e, int on_host) {
 
 int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
-  if (variant < 1 || variant > 3) return fail(CET_E_INVALID, "variant must be 1, 2 or 3");
+  if (variant != 1 && variant != 3) return fail(CET_E_INVALID, "variant must be 1 or 3");
   if (e->kind != 0 && variant != 1) return fail(CET_E_INVALID, "the Transformer engine has one variant");
   e->variant = variant;
   return CET_OK;
@@ -1232,7 +1281,16 @@ int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, f
                    void* stream) {
   if (!pred || !label || !out) return fail(CET_E_INVALID, "null argument");
   if (B <= 0 || T <= 0 || F <= 0 || T > 1024) return fail(CET_E_INVALID, "bad shape");
-  int rc = cet_launch_nmse_split(pred, label, B, T, F, out, nullptr, accumulate, (hipStream_t)stream);
+  int rc = cet_launch_nmse_split(pred, label, B, T, F, out, nullptr, accumulate, nullptr, (hipStream_t)stream);
+  if (rc) return fail(CET_E_HIP, "nmse launch failed");
+  return CET_OK;
+}
+
+int cet_nmse_split_sums(const float* pred, const float* label, int B, int T, int F, float* out, int accumulate,
+                        double* sums, void* stream) {
+  if (!pred || !label || (!out && !sums)) return fail(CET_E_INVALID, "null argument");
+  if (B <= 0 || T <= 0 || F <= 0 || T > 1024) return fail(CET_E_INVALID, "bad shape");
+  int rc = cet_launch_nmse_split(pred, label, B, T, F, out, nullptr, accumulate, sums, (hipStream_t)stream);
   if (rc) return fail(CET_E_HIP, "nmse launch failed");
   return CET_OK;
 }

@@ -239,13 +239,7 @@ extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_
   using namespace cet;
   if (a->B <= 0) return 0;
   auto launch = [&](auto kern) -> int {
-    static bool attr_done = false;  // one per kernel instantiation
-    if (!attr_done) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024) != hipSuccess)
-        return -1;
-      attr_done = true;
-    }
+    if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
     hipLaunchKernelGGL(kern, dim3(a->B), dim3(NTHREADS), lds_bytes, stream, *a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   };

@@ -434,14 +434,8 @@ extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int l
                                       hipStream_t stream) {
   using namespace cet;
   if (a->B <= 0) return 0;
-  static bool attr_done[8] = {};   // one flag per kernel instance
-  auto launch = [&](void (*kern)(InformerArgs, const InformerPlan*), int slot) -> int {
-    if (!attr_done[slot]) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024) != hipSuccess)
-        return -1;
-      attr_done[slot] = true;
-    }
+  auto launch = [&](void (*kern)(InformerArgs, const InformerPlan*), int) -> int {
+    if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
     hipLaunchKernelGGL(kern, dim3(a->B), dim3(v3::NTHREADS), lds_bytes, stream, *a, a->plan);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   };

@@ -14,7 +14,7 @@ struct InformerArgs {
   const void* weights;        // packed bf16 fragment blob
   const float* params;        // fp32 blob: biases, scales, LN, positional tables
   const uint8_t* cnt;         // per-forward ProbSparse key multiplicities (host-built), or
-  const uint32_t* mt_in;      // v2: resident mt19937 state slot to replay the draws from, and
+  const uint32_t* mt_in;      // resident mt19937 state slot to replay the draws from, and
   uint32_t* mt_out;           //     the slot workgroup 0 writes the advanced state to
   uint8_t* cnt_next;          // v3: where the first workgroup to finish writes the next forward's tables
   unsigned* ticket;           // v3: finish counter for that election (the last finisher re-arms it)
@@ -65,10 +65,13 @@ struct TransformerArgs {
   int B;
 };
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, 160 KiB) for `kern` on the CURRENT device,
+// once per (device, kernel); thread-safe (cet_api.cpp).  Returns false if the runtime refuses.
+bool ensure_lds_attr(const void* kern);
+
 }  // namespace cet
 
 extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
-extern "C" int cet_launch_informer_v2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
                                        uint8_t* tab_out, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, int xdec_early,
@@ -77,4 +80,4 @@ extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_nmse_split(const float* pred, const float* label, int B, int T, int F, float* acc,
-                                     float* last, int accumulate, hipStream_t stream);
+                                     float* last, int accumulate, double* sums, hipStream_t stream);

@@ -1,7 +1,8 @@
 // NMSE_Split_cuda (FullPrecision/metrics.py:26-30): per prediction step t,
 //   Σ_{b,f} (x − x̂)² / Σ_{b,f} x̂²   with x̂ = pred (the FIRST argument, as run_validation
 // passes the model output first, QuantizationAwareTraining.py:122).  One workgroup per step,
-// fp64 accumulation, optional running sum (the caller's `loss += ...`).
+// fp64 accumulation, optional running sum (the caller's `loss += ...`), and optionally the raw fp64
+// sums (Σ(x − x̂)², Σx̂²) per step, which ranks holding shards of one batch add up before dividing.
 #include <hip/hip_runtime.h>
 
 #include "cet_kernels.h"
@@ -11,7 +12,8 @@ namespace cet {
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 __global__ void __launch_bounds__(256) nmse_split_kernel(const float* __restrict__ pred, const float* __restrict__ label,
-                                                         int B, int T, int F, float* out, float* last, int accumulate) {
+                                                         int B, int T, int F, float* out, float* last, int accumulate,
+                                                         double* sums) {
   __shared__ double sm[2][4];
   const int t = blockIdx.x;
   double mse = 0.0, pw = 0.0;
@@ -35,8 +37,12 @@ __global__ void __launch_bounds__(256) nmse_split_kernel(const float* __restrict
     double a = 0.0, p = 0.0;
     for (int w = 0; w < 4; ++w) { a += sm[0][w]; p += sm[1][w]; }
     const float r = (float)(a / p);
-    out[t] = accumulate ? out[t] + r : r;
+    if (out) out[t] = accumulate ? out[t] + r : r;
     if (last) last[t] = r;
+    if (sums) {
+      sums[t] = a;
+      sums[T + t] = p;
+    }
   }
 }
 
@@ -45,7 +51,8 @@ __global__ void __launch_bounds__(256) nmse_split_kernel(const float* __restrict
 // b ≡ g (mod nb).  Loads are coalesced float4s, sums fp64 in registers, and the per-t totals
 // are reduced from LDS in a fixed order (deterministic, no atomics).
 __global__ void __launch_bounds__(1024) nmse_split_rows(const float* __restrict__ pred, const float* __restrict__ label,
-                                                        int B, int T, int F, float* out, float* last, int accumulate) {
+                                                        int B, int T, int F, float* out, float* last, int accumulate,
+                                                        double* sums) {
   __shared__ double part[2][1024];
   const int R4 = T * F / 4, nb = 1024 / R4;
   const int j = threadIdx.x % R4, g = threadIdx.x / R4;
@@ -111,8 +118,12 @@ __global__ void __launch_bounds__(1024) nmse_split_rows(const float* __restrict_
     }
     if (lane == 0) {
       const float r = (float)(a / p);
-      out[t] = accumulate ? out[t] + r : r;
+      if (out) out[t] = accumulate ? out[t] + r : r;
       if (last) last[t] = r;
+      if (sums) {
+        sums[t] = a;
+        sums[T + t] = p;
+      }
     }
   }
 }
@@ -120,13 +131,13 @@ __global__ void __launch_bounds__(1024) nmse_split_rows(const float* __restrict_
 }  // namespace cet
 
 extern "C" int cet_launch_nmse_split(const float* pred, const float* label, int B, int T, int F, float* acc,
-                                     float* last, int accumulate, hipStream_t stream) {
+                                     float* last, int accumulate, double* sums, hipStream_t stream) {
   const bool aligned = ((reinterpret_cast<uintptr_t>(pred) | reinterpret_cast<uintptr_t>(label)) & 15) == 0;
   if (aligned && F % 4 == 0 && T * F / 4 <= 1024)
     hipLaunchKernelGGL(cet::nmse_split_rows, dim3(1), dim3(1024), 0, stream, pred, label, B, T, F, acc, last,
-                       accumulate);
+                       accumulate, sums);
   else
     hipLaunchKernelGGL(cet::nmse_split_kernel, dim3(T), dim3(256), 0, stream, pred, label, B, T, F, acc, last,
-                       accumulate);
+                       accumulate, sums);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

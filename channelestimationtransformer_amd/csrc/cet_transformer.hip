@@ -161,14 +161,8 @@ __global__ void __launch_bounds__(NTHREADS, 1) transformer_forward(TransformerAr
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
   using namespace cet;
   if (a->B <= 0) return 0;
-  static bool attr_done[2] = {false, false};   // one flag per kernel instance
-  auto launch = [&](void (*kern)(TransformerArgs, const TransformerPlan*), int slot) -> int {
-    if (!attr_done[slot]) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024) != hipSuccess)
-        return -1;
-      attr_done[slot] = true;
-    }
+  auto launch = [&](void (*kern)(TransformerArgs, const TransformerPlan*), int) -> int {
+    if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
     hipLaunchKernelGGL(kern, dim3(a->B), dim3(NTHREADS), lds_bytes, stream, *a, a->plan);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   };

@@ -89,6 +89,17 @@ class Engine:
             k += lq * u
         return out
 
+    def peek_draw(self) -> List[np.ndarray]:
+        """The draws the next native forward will consume, without advancing the stream."""
+        n = check(lib.cet_peek_draw(self._h, None, 0), "cet_peek_draw")
+        buf = np.empty(max(n, 1), dtype=np.int32)
+        check(lib.cet_peek_draw(self._h, buf.ctypes.data_as(ctypes.c_void_p), n), "cet_peek_draw")
+        out, k = [], 0
+        for _, (lq, u) in self.prob_calls():
+            out.append(buf[k:k + lq * u].reshape(lq, u))
+            k += lq * u
+        return out
+
     def seed(self, seed: int) -> None:
         check(lib.cet_seed(self._h, ctypes.c_uint64(int(seed) & (2 ** 64 - 1))), "cet_seed")
 
@@ -122,7 +133,7 @@ class Engine:
         check(lib.cet_set_sampler(self._h, int(bool(on_host))), "cet_set_sampler")
 
     def set_variant(self, variant: int) -> None:
-        """Fused-kernel generation: 2 (register-resident, default) or 1 (LDS-resident)."""
+        """Fused-kernel generation: 3 (register-resident, default) or 1 (LDS-resident)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
 
     # ------------------------------------------------------------------ kernel timing
@@ -155,15 +166,45 @@ def nmse_split(pred, label, out=None, accumulate: bool = False, stream: Optional
     """Device NMSE_Split_cuda(pred, label) → fp32 tensor [T] (FullPrecision/metrics.py:26-30)."""
     import torch
 
+    if pred.dim() != 3 or tuple(label.shape) != tuple(pred.shape):
+        raise ValueError(f"pred and label must both be [B, T, F]; got {tuple(pred.shape)} and {tuple(label.shape)}")
+    for name, t in (("pred", pred), ("label", label)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != pred.device or not t.is_cuda:
+            raise ValueError(f"{name} must be a contiguous float32 tensor on the same HIP device")
     B, T, F = pred.shape
     if out is None:
         out = torch.zeros(T, dtype=torch.float32, device=pred.device)
+    elif out.dtype != torch.float32 or out.numel() != T or out.device != pred.device or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous float32 tensor of {T} elements on {pred.device}")
     if stream is None:
         stream = _stream_ptr(pred.device)
     check(lib.cet_nmse_split(ctypes.c_void_p(pred.data_ptr()), ctypes.c_void_p(label.data_ptr()), B, T, F,
                              ctypes.c_void_p(out.data_ptr()), int(accumulate), ctypes.c_void_p(stream)),
           "cet_nmse_split")
     return out
+
+
+def nmse_split_sums(pred, label, sums, out=None, accumulate: bool = False, stream: Optional[int] = None):
+    """Raw fp64 NMSE_Split sums of one batch into ``sums`` (float64 [2, T]: Σ(x−x̂)², Σx̂² per step), and
+    optionally the ratio into ``out`` as :func:`nmse_split` does."""
+    import torch
+
+    if pred.dim() != 3 or tuple(label.shape) != tuple(pred.shape):
+        raise ValueError(f"pred and label must both be [B, T, F]; got {tuple(pred.shape)} and {tuple(label.shape)}")
+    for name, t in (("pred", pred), ("label", label)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != pred.device or not t.is_cuda:
+            raise ValueError(f"{name} must be a contiguous float32 tensor on the same HIP device")
+    B, T, F = pred.shape
+    if sums.dtype != torch.float64 or sums.numel() != 2 * T or sums.device != pred.device or not sums.is_contiguous():
+        raise ValueError(f"sums must be a contiguous float64 tensor of {2 * T} elements on {pred.device}")
+    if out is not None and (out.dtype != torch.float32 or out.numel() != T or out.device != pred.device):
+        raise ValueError(f"out must be a float32 tensor of {T} elements on {pred.device}")
+    if stream is None:
+        stream = _stream_ptr(pred.device)
+    check(lib.cet_nmse_split_sums(ctypes.c_void_p(pred.data_ptr()), ctypes.c_void_p(label.data_ptr()), B, T, F,
+                                  ctypes.c_void_p(out.data_ptr()) if out is not None else None, int(accumulate),
+                                  ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(stream)), "cet_nmse_split_sums")
+    return sums
 
 
 def _to_numpy(v):

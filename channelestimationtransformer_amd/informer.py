@@ -56,7 +56,10 @@ class _EngineModule(nn.Module):
         self._engine: Optional[Engine] = None
         self._engine_device = None
         self._synced_version = None
-        self.native_rng_seed: Optional[int] = None   # None: draw from torch's global generator
+        # None: draw from torch's global generator (the reference protocol).  An int: the engine's
+        # native torch-compatible sampler, seeded with it once (re-seeded when the value changes).
+        self.native_rng_seed: Optional[int] = None
+        self._applied_seed: Optional[int] = None
 
     def _make_engine(self) -> Engine:  # pragma: no cover - abstract
         raise NotImplementedError
@@ -73,6 +76,7 @@ class _EngineModule(nn.Module):
                 self._engine = self._make_engine()
             self._engine_device = device
             self._synced_version = None
+            self._applied_seed = None
         v = self._version()
         if v != self._synced_version:
             self._engine.load_state_dict(self.state_dict())
@@ -95,7 +99,8 @@ class LazyAttns(_Seq):
 
     Materialising them costs ~346 KB of HBM writes per sequence, so they are
     produced only when first indexed, by replaying the same forward (same inputs, same
-    ProbSparse draws) with the attention-map output enabled.
+    ProbSparse draws — recorded before the forward in native-sampler mode, so the replay
+    neither re-draws nor moves the stream) with the attention-map output enabled.
     """
 
     def __init__(self, producer, n_enc, layers_per_enc, stack):
@@ -200,6 +205,13 @@ class InformerStack(_EngineModule):
             if self.native_rng_seed is None:
                 idx = draw_indices(eng.prob_calls())       # global generator, reference call order
                 eng.set_indices(idx)
+            else:
+                if self._applied_seed != self.native_rng_seed:
+                    eng.seed(self.native_rng_seed)
+                    self._applied_seed = self.native_rng_seed
+                if self.output_attention and not self.materialize_attns:
+                    # the lazy maps replay this forward: record its draws (the stream does not move)
+                    idx = eng.peek_draw()
         out = torch.empty(B, self.pred_len, self.c_out, device=dev, dtype=torch.float32)
         attn_buf = None
         if self.output_attention and self.materialize_attns:

@@ -7,9 +7,13 @@ at every SNR of ``SNR.sbatch`` (:9-13: 12, 14, 16, 18, 20 dB), with the whole da
 drop_last=True)``: one seeded permutation per SNR, whole batches only, and the reported loss is the
 mean of the per-batch ratios (``loss / len(val_dataloader)``).
 
-Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N -m channelestimationtransformer_amd.sweep``.
-Every rank holds whole reference batches of ``--batch`` sequences; the per-batch ratio sums are
-all-reduced over RCCL at the end of each SNR (no collective in the data path).
+Multi-GPU (config C4: a reference batch of 4096 = 8 × 512 sharded over 8 GPUs):
+``python -m channelestimationtransformer_amd.sweep --gpus N`` starts N ranks itself (or run it under
+torchrun).  Reference batch i is the N shards of ``--batch`` sequences the ranks take from the loader's
+permutation at step i.  Each rank keeps the raw fp64 NMSE_Split sums of its shard per step; at the end
+of an SNR one all_reduce turns them into each global batch's ratio (``NMSE_Split_cuda`` over all
+N × batch predictions) and one all_gather collates the last batch's predictions on rank 0, which
+reduces NMSE_Split over them and checks the all-reduced value (no collective in the data path).
 
 Data: ``--dataset`` (a ``.npy`` complex ``[N, slots, 2, 4]``, or a ``.pt`` tensor read with
 ``weights_only=True``) or, by default, seeded Jakes channels generated on the device.  Weights:
@@ -68,8 +72,9 @@ def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=Non
     """Yields one result dict per SNR (identical on every rank)."""
     import torch
 
-    from .engine import nmse_split
+    from .engine import nmse_split, nmse_split_sums
     from .pipeline import DeviceSeqData, synth_channels
+    from .sharding import check_gathered_nmse, collate_step_sums, gather_predictions
 
     c = CONFIG
     model = build_model(device, checkpoint)
@@ -92,7 +97,7 @@ def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=Non
     for k, snr in enumerate(snrs):
         g = torch.Generator().manual_seed(seed * 1000 + k)
         perm = torch.randperm(len(data), generator=g).to(torch.int32).to(device)   # the loader's shuffle
-        acc = torch.zeros(c["pred_len"], device=device)
+        sums = torch.zeros(n_batches, 2, c["pred_len"], dtype=torch.float64, device=device)
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for i in range(n_batches):
@@ -100,34 +105,46 @@ def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=Non
             xe, xd, lb = data.batch(idx=perm[off:off + batch], seed=seed, counter=(k << 32) + i * world + rank,
                                     snr=snr, out=bufs, stream=stream)
             eng.forward(xe, xd, out, None, stream)
-            nmse_split(out, lb, acc, accumulate=True, stream=stream)
+            nmse_split_sums(out, lb, sums[i], stream=stream)
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
-        tot = acc.double()
-        cnt = torch.tensor([float(n_batches)], device=device, dtype=torch.float64)
         if dist is not None:
-            dist.all_reduce(tot)
-            dist.all_reduce(cnt)
             t = torch.tensor([dt], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        nmse = (tot / cnt).cpu().numpy()
+        ratios, nmse = collate_step_sums(sums, world)
+        preds, labels = gather_predictions(out, world), gather_predictions(bufs[2], world)
+        check = None
+        if rank == 0:
+            g = nmse_split(torch.cat(preds).contiguous(), torch.cat(labels).contiguous())
+            check = check_gathered_nmse(g, ratios[-1])
+        nmse = nmse.cpu().numpy()
         seqs = n_batches * batch * world
         yield {"snr": snr, "nmse": [float(v) for v in nmse], "nmse_db": [round(float(10 * np.log10(v)), 4) for v in nmse],
-               "nmse_db_mean": round(float(10 * np.log10(nmse.mean())), 4), "batches": int(cnt.item()),
-               "sequences": seqs, "seconds": round(dt, 4), "seq_per_s": round(seqs / dt, 1)}
+               "nmse_db_mean": round(float(10 * np.log10(nmse.mean())), 4), "batches": n_batches,
+               "global_batch": batch * world, "sequences": seqs, "seconds": round(dt, 4),
+               "seq_per_s": round(seqs / dt, 1), "world": world, "nmse_gathered_vs_allreduced_rel": check}
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--snr", type=float, nargs="+", default=[12, 14, 16, 18, 20])
-    ap.add_argument("--batch", type=int, default=512, help="reference batch (sequences per rank per step)")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks to start (one process per GPU)")
+    ap.add_argument("--batch", type=int, default=512, help="sequences per rank per step (the reference batch is "
+                                                            "--batch x ranks)")
     ap.add_argument("--batches", type=int, default=8, help="batches per rank per SNR (0: one epoch)")
     ap.add_argument("--samples", type=int, default=None, help="synthetic dataset size (default: exactly the batches)")
     ap.add_argument("--dataset", default=None)
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args(argv)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        import sys
+
+        from .sharding import spawn_ranks
+
+        rest = list(argv) if argv is not None else sys.argv[1:]
+        raise SystemExit(spawn_ranks(args.gpus, ["channelestimationtransformer_amd.sweep"] + rest, module=True))
 
     import torch
 

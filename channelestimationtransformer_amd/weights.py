@@ -38,8 +38,9 @@ def _fan_in(shape: Tuple[int, ...]) -> int:
     return int(np.prod(shape[1:])) if len(shape) > 1 else int(shape[0])
 
 
-def synthetic_state_dict(spec: Iterable[Entry], seed: int = 0) -> Dict[str, np.ndarray]:
-    """Deterministic state dict for ``spec`` (numpy arrays, float32 / int64)."""
+def synthetic_state_dict(spec: Iterable[Entry], seed: int = 0, lsq_bits: int = 8) -> Dict[str, np.ndarray]:
+    """Deterministic state dict for ``spec`` (numpy arrays, float32 / int64); LSQ step sizes (if the
+    schema has them) are the ``lsq_bits`` initialisation of LSQ.py:54-58."""
     spec = list(spec)
     shapes = {k: s for k, s, _ in spec}
     rng = np.random.default_rng(seed)
@@ -73,7 +74,7 @@ def synthetic_state_dict(spec: Iterable[Entry], seed: int = 0) -> Dict[str, np.n
         out[key] = np.ascontiguousarray(v, dtype=np.float32)
     steps = [k for k, _, kind in spec if kind == "step"]
     if steps:
-        out.update(lsq_step_sizes(out, steps, nbits=8))
+        out.update(lsq_step_sizes(out, steps, nbits=lsq_bits))
     return out
 
 

@@ -80,12 +80,17 @@ int cet_missing_weights(cet_engine* e, char* first_missing, int buflen);
 /* ProbSparse sampling.  cet_prob_calls() returns the number of torch.randint draws one
  * forward makes; shapes[i*3..] = {L_K, L_Q, U} for i < max. */
 int cet_prob_calls(cet_engine* e, int* shapes, int max);
+/* Explicit draws for the NEXT forward only (parity mode); all calls must be set.  They are consumed
+ * by that forward and leave a seeded native stream where it was. */
 int cet_set_prob_indices(cet_engine* e, int call, const int32_t* host_idx, int L_Q, int U);
 int cet_seed(cet_engine* e, uint64_t seed);          /* switch to the native sampler */
 /* Draw one forward's worth of indices (all calls, concatenated, row-major) from the native
  * sampler into host memory, advancing it exactly as cet_forward would; returns the count
  * (out == NULL: only the count). */
 int64_t cet_native_draw(cet_engine* e, int32_t* out, int64_t n_max);
+/* The draws the NEXT native forward will consume (same layout as cet_native_draw) without
+ * advancing the stream: lets a caller replay that forward later with explicit indices. */
+int64_t cet_peek_draw(cet_engine* e, int32_t* out, int64_t n_max);
 
 /* Forward on device buffers: x_enc [B][seq_len][enc_in], x_dec [B][label_len+out_len][dec_in]
  * → out [B][out_len][c_out].  attns (optional, Informer with output_attention): per
@@ -99,15 +104,15 @@ int cet_attns_layout(cet_engine* e, int64_t* offsets, int* lengths, int max);
 int cet_set_debug(cet_engine* e, float* dbg_dev);
 int64_t cet_debug_floats(cet_engine* e);
 int cet_debug_layout(cet_engine* e, char* json, int buflen);
-/* Diagnostics (v2 kernel): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
+/* Diagnostics (DIAG kernel instance): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
 
 /* Select the fused-kernel generation of an Informer engine: 3 (default, 8-wave register-resident,
- * two sequences per CU), 2 (4-wave register-resident) or 1 (LDS-resident, one sequence per CU).
+ * two sequences per CU) or 1 (LDS-resident, one sequence per CU).
  * CET_KERNEL=v1 in the environment selects 1 at creation. */
 int cet_set_variant(cet_engine* e, int variant);
 
-/* Where the native sampler (after cet_seed) runs for variants 2/3: 0 = on the device (the
+/* Where the native sampler (after cet_seed) runs for variant 3: 0 = on the device (the
  * resident mt19937, default), 1 = on the host (the same torch-compatible stream drawn by the host
  * mirror, the multiplicity tables staged per forward through a pinned ring and copied on the
  * caller's stream ahead of the kernel).  Both give identical draws; switching keeps the stream.
@@ -125,6 +130,11 @@ int cet_timing_read(cet_engine* e, double* total_ms, int64_t* launches);
  * tensors → out_dev[T] (fp32); if accumulate, out_dev[T] += ratio instead of =. */
 int cet_nmse_split(const float* pred, const float* label, int B, int T, int F, float* out_dev, int accumulate,
                    void* stream);
+/* The same reduction with its raw fp64 sums: sums_dev[t] = Σ_{b,f}(x − x̂)², sums_dev[T + t] = Σ_{b,f} x̂²
+ * (overwritten), so ranks that hold shards of one batch can add their sums before dividing.  out_dev
+ * (may be NULL) receives / accumulates the ratio as cet_nmse_split does. */
+int cet_nmse_split_sums(const float* pred, const float* label, int B, int T, int F, float* out_dev, int accumulate,
+                        double* sums_dev, void* stream);
 
 /* Device channel pipeline.  For b < B, sample s = sample_idx ? sample_idx[b] : sample_base + b of
  * the complex64 dataset [n_samples][slots][nr][nt] (interleaved re, im): normalise to unit mean

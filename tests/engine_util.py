@@ -9,7 +9,7 @@ from golden_util import Case, oracle_for, rel_nmse
 
 def model_for(case: Case):
     """The engine mirror constructed exactly as the reference callers construct the reference."""
-    from channelestimationtransformer_amd.informer import InformerStack, InformerStackLSQ
+    from channelestimationtransformer_amd.informer import Informer, InformerStack, InformerStackLSQ
     from channelestimationtransformer_amd.transformer import build_transformer
 
     cfg = case.cfg
@@ -26,6 +26,8 @@ def model_for(case: Case):
         if kind == "informer_lsq":
             m = InformerStackLSQ(*args, cfg["num_bits"])
             m.enable_lsq(cfg["num_bits"])
+        elif kind == "informer":
+            m = Informer(*args)
         else:
             m = InformerStack(*args)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in case.state.items()}, strict=True)

@@ -52,8 +52,14 @@ CASES = {
     "informer_prob_seq48": dict(model="informer_stack", cfg=dict(seq_len=48), B=2, acts=False),
     # C3: build_transformer(16,16,90,5,10,128,3,8,0.05,64)
     "transformer_c3": dict(model="transformer", cfg={}, B=4, acts=True),
-    # C5: LSQ 8-bit weights (models/InformerLSQ)
+    # C5: LSQ 8-bit weights (models/InformerLSQ); the LSQ study sweeps 8..11 bits
+    # (QuantizationStudy/LSQ/TrainInformerLSQ.py:338)
     "informer_lsq8": dict(model="informer_lsq", cfg=dict(num_bits=8), B=2, acts=False),
+    "informer_lsq9": dict(model="informer_lsq", cfg=dict(num_bits=9), B=2, acts=False),
+    "informer_lsq10": dict(model="informer_lsq", cfg=dict(num_bits=10), B=2, acts=False),
+    "informer_lsq11": dict(model="informer_lsq", cfg=dict(num_bits=11), B=2, acts=False),
+    # single-encoder Informer (FullPrecision/InformerModel/model.py:11-139), e_layers an int
+    "informer_single_e3": dict(model="informer", cfg=dict(e_layers=3), B=2, acts=True),
 }
 
 
@@ -74,6 +80,16 @@ def build_reference(kind, cfg):
                           cfg["d_layers"], cfg["d_ff"], cfg["dropout"], cfg["attn"], cfg["embed"],
                           cfg["activation"], cfg["output_attention"], cfg["distil"], dev)
         return m, _informer_schema(cfg)
+    if kind == "informer":
+        sys.path.insert(0, os.path.join(REF, "FullPrecision"))
+        from InformerModel.model import Informer
+        m = Informer(cfg["enc_in"], cfg["dec_in"], cfg["c_out"], cfg["seq_len"], cfg["label_len"],
+                     cfg["pred_len"], cfg["factor"], cfg["d_model"], cfg["n_heads"], cfg["e_layers"],
+                     cfg["d_layers"], cfg["d_ff"], cfg["dropout"], cfg["attn"], cfg["embed"],
+                     cfg["activation"], cfg["output_attention"], cfg["distil"], dev)
+        return m, S.informer_spec(cfg["enc_in"], cfg["dec_in"], cfg["c_out"], cfg["d_model"], cfg["n_heads"],
+                                  cfg["e_layers"], cfg["d_layers"], cfg["d_ff"], embed=cfg["embed"],
+                                  freq=cfg["activation"], distil=True)
     if kind == "informer_lsq":
         sys.path.insert(0, REF)
         from models.InformerLSQ.model import InformerStack
@@ -110,7 +126,7 @@ def run_case(name, c):
     kind = c["model"]
     model, schema = build_reference(kind, cfg)
     weight_seed = 0
-    state = synthetic_state_dict(schema, seed=weight_seed)
+    state = synthetic_state_dict(schema, seed=weight_seed, lsq_bits=cfg.get("num_bits", 8))
     if kind == "informer_lsq":
         lsq_enable(model, cfg["num_bits"], state)
     ref_keys = list(model.state_dict().keys())
@@ -130,8 +146,22 @@ def run_case(name, c):
             acts[tag] = o.detach().numpy().astype(np.float32)
         return f
 
+    if kind == "informer":
+        mods = dict(model.named_modules())
+        hooks.append(model.enc_embedding.register_forward_hook(hook("enc_emb")))
+        enc = model.encoder
+        for l, lay in enumerate(enc.attn_layers):
+            hooks.append(lay.register_forward_hook(hook(f"enc0_layer{l}", 0)))
+        if enc.conv_layers is not None:
+            for l, cl in enumerate(enc.conv_layers):
+                hooks.append(cl.register_forward_hook(hook(f"enc0_conv{l}")))
+        hooks.append(enc.register_forward_hook(hook("enc0_out", 0)))
+        hooks.append(model.dec_embedding.register_forward_hook(hook("dec_emb")))
+        for l, lay in enumerate(model.decoder.layers):
+            hooks.append(lay.register_forward_hook(hook(f"dec_layer{l}")))
+        hooks.append(model.decoder.register_forward_hook(hook("dec_out")))
+        hooks.append(model.projection.register_forward_hook(hook("proj")))
     if kind in ("informer_stack", "informer_lsq"):
-        from importlib import import_module
         mods = dict(model.named_modules())
         hooks.append(model.enc_embedding.register_forward_hook(hook("enc_emb")))
         for i, enc in enumerate(model.encoder.encoders):
@@ -147,6 +177,7 @@ def run_case(name, c):
             hooks.append(lay.register_forward_hook(hook(f"dec_layer{l}")))
         hooks.append(model.decoder.register_forward_hook(hook("dec_out")))
         hooks.append(model.projection.register_forward_hook(hook("proj")))
+    if kind != "transformer":
         for n, mod in mods.items():
             if type(mod).__name__ == "ProbAttention":
                 orig = mod._prob_QK
@@ -156,7 +187,7 @@ def run_case(name, c):
                     mtops.append(np.sort(mt.numpy(), axis=-1).astype(np.int32))
                     return qk, mt
                 mod._prob_QK = wrapped
-    else:
+    if kind == "transformer":
         hooks.append(model.src_pos.register_forward_hook(hook("enc_emb")))
         for l, lay in enumerate(model.encoder.layers):
             hooks.append(lay.register_forward_hook(hook(f"enc_layer{l}")))
@@ -205,6 +236,8 @@ def run_case(name, c):
         for k, v in acts.items():
             res[f"act_{k}"] = v
         if attns is not None:
+            if kind == "informer":          # Informer returns one encoder's per-layer maps
+                attns = [attns]
             for i, enc_attns in enumerate(attns):
                 for l, a in enumerate(enc_attns):
                     if a is not None:

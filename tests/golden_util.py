@@ -43,21 +43,21 @@ def load_case(name: str) -> Case:
         z = {k: f[k] for k in f.files}
     meta = json.loads(str(z.pop("meta")))
     spec = [(k, tuple(s), kd) for k, s, kd in meta["keys"]]
-    state = synthetic_state_dict(spec, meta["weight_seed"])
+    state = synthetic_state_dict(spec, meta["weight_seed"], lsq_bits=meta["cfg"].get("num_bits", 8))
     idx = [z[f"idx{k}"] for k in range(meta["n_randint"])]
     return Case(name, meta, z, state, idx)
 
 
-def informer_oracle_config(cfg: dict, lsq_bits=None):
+def informer_oracle_config(cfg: dict, lsq_bits=None, stack=True):
     """Effective oracle flags for the callers' 19/20-positional-argument construction."""
     from oracle.informer_np import InformerConfig
 
     return InformerConfig(enc_in=cfg["enc_in"], dec_in=cfg["dec_in"], c_out=cfg["c_out"], seq_len=cfg["seq_len"],
                           label_len=cfg["label_len"], pred_len=cfg["pred_len"], factor=cfg["factor"],
-                          d_model=cfg["d_model"], n_heads=cfg["n_heads"], e_layers=tuple(cfg["e_layers"]),
+                          d_model=cfg["d_model"], n_heads=cfg["n_heads"], e_layers=tuple(cfg["e_layers"]) if stack else (int(cfg["e_layers"]),),
                           d_layers=cfg["d_layers"], d_ff=cfg["d_ff"], attn=cfg["attn"],
                           activation="gelu" if cfg["output_attention"] != "relu" else "relu",
-                          output_attention=bool(cfg["distil"]), distil=True, mix=True, stack=True,
+                          output_attention=bool(cfg["distil"]), distil=True, mix=True, stack=stack,
                           lsq_bits=lsq_bits)
 
 
@@ -71,7 +71,8 @@ def oracle_for(case: Case, dtype=np.float64):
                                cfg["d_layers"], cfg["n_heads"], cfg["d_ff"])
         return TransformerOracle(tc, case.state, dtype)
     bits = cfg.get("num_bits") if case.meta["model"] == "informer_lsq" else None
-    return InformerOracle(informer_oracle_config(cfg, bits), case.state, dtype)
+    return InformerOracle(informer_oracle_config(cfg, bits, stack=case.meta["model"] != "informer"), case.state,
+                          dtype)
 
 
 def rel_nmse(a, b):

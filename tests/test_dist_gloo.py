@@ -89,3 +89,86 @@ def test_two_rank_collation_matches_unsharded():
     np.testing.assert_allclose(preds, ref_preds, rtol=1e-12, atol=1e-12)
     ref = np.mean([nmse_split(ref_preds[b:b + 2], lab[b:b + 2]) for b in range(0, 8, 2)], axis=0)
     np.testing.assert_allclose(nmse, ref, rtol=1e-12)
+
+
+def test_bench_spawns_its_ranks_and_collates_by_gather():
+    """`python bench.py --gpus 2` starts its two ranks itself (torch.distributed.run child, gloo here via
+    --collation-selftest): the per-step sums are all-reduced, rank 0 all-gathers the last step's
+    predictions and its NMSE_Split over them equals the all-reduced value; the mean of per-step
+    global ratios equals the unsharded computation."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--collation-selftest",
+                        "--steps", "3", "--batch", "8"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, r.stdout
+    res = json.loads(line[0])
+    assert res["world"] == 2 and res["backend"] == "gloo" and res["global_batch"] == 16
+    assert res["gathered_vs_allreduced_rel"] < 1e-12
+    # unsharded reference: the same stand-in predictions of both ranks, one ratio per global step
+    T, steps = 5, 3
+    labs, outs = [], [[] for _ in range(steps)]
+    for rank in range(2):
+        g = torch.Generator().manual_seed(1234 + 7919 * rank)
+        lab = torch.randn(8, T, 16, generator=g)
+        labs.append(lab)
+        for s in range(steps):
+            outs[s].append(lab + 0.1 * (s + 1) * torch.randn(8, T, 16, generator=g))
+    from channelestimationtransformer_amd.sharding import nmse_split_torch
+
+    lab = torch.cat(labs)
+    ref = torch.stack([nmse_split_torch(torch.cat(outs[s]), lab) for s in range(steps)]).mean(0)
+    np.testing.assert_allclose(res["nmse"], ref.numpy(), rtol=1e-12)
+
+
+def test_step_sum_collation_two_ranks():
+    """collate_step_sums over gloo: global per-step ratios from per-rank sums."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sums_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ratios, nmse = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from channelestimationtransformer_amd.sharding import nmse_split_torch
+
+    preds, labs = _sums_data()
+    ref = torch.stack([nmse_split_torch(torch.cat([preds[0][s], preds[1][s]]), torch.cat(labs)) for s in range(4)])
+    np.testing.assert_allclose(ratios, ref.numpy(), rtol=1e-12)
+    np.testing.assert_allclose(nmse, ref.mean(0).numpy(), rtol=1e-12)
+
+
+def _sums_data():
+    g = torch.Generator().manual_seed(5)
+    labs = [torch.randn(6, 5, 16, generator=g) for _ in range(2)]
+    preds = [[labs[r] + torch.randn(6, 5, 16, generator=g) for _ in range(4)] for r in range(2)]
+    return preds, labs
+
+
+def _sums_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from channelestimationtransformer_amd.sharding import collate_step_sums
+
+        preds, labs = _sums_data()
+        sums = torch.zeros(4, 2, 5, dtype=torch.float64)
+        for s in range(4):
+            p = preds[rank][s].double()
+            d = labs[rank].double() - p
+            sums[s, 0], sums[s, 1] = (d * d).sum((0, 2)), (p * p).sum((0, 2))
+        ratios, nmse = collate_step_sums(sums, world)
+        if rank == 0:
+            q.put((ratios.numpy(), nmse.numpy()))
+    finally:
+        dist.destroy_process_group()

@@ -39,6 +39,8 @@ def test_oracle_matches_reference(name):
         assert len(trace.m_top) == n
         for k in range(n):
             np.testing.assert_array_equal(trace.m_top[k], case.z[f"mtop{k}"])
+        if case.meta["model"] == "informer":     # Informer returns one encoder's per-layer maps
+            attns = [attns]
         for key, a in case.z.items():
             if key.startswith("attn_e"):
                 e, l = key[6:].split("_l")
@@ -57,3 +59,28 @@ def test_index_draws_are_torch_randint():
         got = draw_indices(shapes, seed=case.meta["rng_seed"])
         for g, i in zip(got, case.idx):
             np.testing.assert_array_equal(g, i)
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if n.startswith("informer")])
+def test_torch_restatement_matches_reference(name):
+    """oracle/informer_torch.py (the CPU baseline's forward: the reference's own aten ops) in float64
+    against the reference fixtures."""
+    import torch
+
+    from golden_util import informer_oracle_config
+    from oracle.informer_torch import TorchInformer
+
+    case = load_case(name)
+    bits = case.cfg.get("num_bits") if case.meta["model"] == "informer_lsq" else None
+    cfg = informer_oracle_config(case.cfg, bits, stack=case.meta["model"] != "informer")
+    m = TorchInformer(cfg, case.state, dtype=torch.float64)
+    out = m.forward(torch.from_numpy(case.z["x_enc"]).double(), torch.from_numpy(case.z["x_dec"]).double(),
+                    case.idx).numpy()
+    assert rel_nmse(out, case.z["out"]) < 1e-10, rel_nmse(out, case.z["out"])
+
+
+def test_host_cpu_description():
+    from oracle.informer_torch import host_cpu
+
+    h = host_cpu()
+    assert h["usable_logical"] >= 1 and isinstance(h["model"], str)
