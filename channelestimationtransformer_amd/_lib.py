@@ -48,6 +48,8 @@ def _load():
         "cet_native_draw": (c_int64, [c_void_p, c_void_p, c_int64]),
         "cet_peek_draw": (c_int64, [c_void_p, c_void_p, c_int64]),
         "cet_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+        "cet_forward_nmse": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
         "cet_attns_floats": (c_int64, [c_void_p]),
         "cet_attns_layout": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int), c_int]),
         "cet_set_debug": (c_int, [c_void_p, c_void_p]),
@@ -59,6 +61,8 @@ def _load():
         "cet_timing": (c_int, [c_void_p, c_int]),
         "cet_set_variant": (c_int, [c_void_p, c_int]),
         "cet_set_sampler": (c_int, [c_void_p, c_int]),
+        "cet_set_precision": (c_int, [c_void_p, c_int]),
+        "cet_get_precision": (c_int, [c_void_p]),
         "cet_set_stamps": (c_int, [c_void_p, c_void_p]),
         "cet_timing_read": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
         "cet_prepare_batch": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_void_p,
@@ -78,9 +82,9 @@ lib = _load()
 EXPORTED = ("cet_last_error", "cet_version", "cet_create_informer", "cet_create_transformer", "cet_destroy",
             "cet_load_weight", "cet_missing_weights", "cet_prob_calls", "cet_set_prob_indices", "cet_seed",
             "cet_native_draw", "cet_peek_draw",
-            "cet_forward", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
+            "cet_forward", "cet_forward_nmse", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
             "cet_debug_layout", "cet_nmse_split", "cet_nmse_split_sums", "cet_timing", "cet_timing_read",
-            "cet_set_variant", "cet_set_sampler", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
+            "cet_set_variant", "cet_set_sampler", "cet_set_precision", "cet_get_precision", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
 
 
 def check(rc: int, what: str = "") -> int:

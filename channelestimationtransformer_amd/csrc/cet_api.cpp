@@ -82,8 +82,34 @@ uint16_t f2bf(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+float bf2f(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+// OCP e4m3fn (gfx950's fp8), round-half-even, saturating at ±448 (the packer only feeds it values it
+// represents exactly: integers of magnitude ≤ 16 and multiples of 16 up to 128)
+uint8_t f2e4m3(float f) {
+  const uint8_t s = std::signbit(f) ? 0x80 : 0;
+  const double a = std::fabs((double)f);
+  if (a == 0.0) return s;
+  int e2;
+  const double m = std::frexp(a, &e2);   // a = m·2^e2, m ∈ [0.5, 1)
+  int E = e2 - 1 + 7;                    // a = (2m)·2^(e2-1)
+  if (E >= 1) {
+    int mant = (int)std::nearbyint((2.0 * m - 1.0) * 8.0);
+    if (mant == 8) { mant = 0; ++E; }
+    if (E > 15 || (E == 15 && mant > 6)) return (uint8_t)(s | 0x7e);
+    return (uint8_t)(s | (E << 3) | mant);
+  }
+  int mant = (int)std::nearbyint(a * 512.0);   // subnormal: mant·2^-9
+  if (mant >= 8) return (uint8_t)(s | (1 << 3));
+  return (uint8_t)(s | mant);
+}
 
 int r16(int x) { return (x + 15) & ~15; }
+constexpr int MT_WORDS_HOST = 640;   // cet_mt.hpp MT_WORDS (state + index, padded)
 int r32(int x) { return (x + 31) & ~31; }
 int u_part(int factor, int L) {
   const int u = factor * (int)std::ceil(std::log((double)L));
@@ -107,10 +133,13 @@ struct cet_engine {
   std::vector<std::string> order;
   bool dirty = true;
   bool uploaded = false;
-  int variant = 3;   // fused-kernel generation (CET_KERNEL=v1 selects the LDS-resident kernel)
+  int variant = 4;   // fused-kernel generation (CET_KERNEL=v1 / v3 select the older kernels)
 
   // packed blobs
   std::vector<uint16_t> wblob;
+  std::vector<uint16_t> wblob_lo;   // v4 split-bf16: lo fragments (uploaded after wblob)
+  int prec_req = -1;                // cet_set_precision: -1 auto, else v4::P_BF16 / P_X3 / P_FP8
+  int prec = 0;                     // the precision the plan was built for
   std::vector<float> pblob;
   InformerPlan ip{};
   TransformerPlan tp{};
@@ -149,6 +178,8 @@ struct cet_engine {
   int tab_cur = 0;
   bool tab_ready = false;
   unsigned* d_ticket = nullptr;
+  float2* d_nmse_part = nullptr;   // fused NMSE: per-sequence partials [B][pred_len]
+  size_t nmse_part_n = 0;
   static constexpr int PREP_MIN_B = 64;   // below this the first finisher has no slack to hide in
 
   // per-forward multiplicity tables (ring of pinned staging + device buffers)
@@ -185,6 +216,7 @@ struct cet_engine {
     for (auto* t : d_tab)
       if (t) (void)hipFree(t);
     if (d_ticket) (void)hipFree(d_ticket);
+    if (d_nmse_part) (void)hipFree(d_nmse_part);
     if (h_mt) (void)hipHostFree(h_mt);
     if (ev_mt) (void)hipEventDestroy(ev_mt);
   }
@@ -327,8 +359,10 @@ void schema_transformer(cet_engine* e) {
 struct Packer {
   std::vector<uint16_t>& wb;
   std::vector<float>& pb;
+  std::vector<uint16_t>* wlo = nullptr;   // split-bf16 (v4 P_X3): the lo fragments, parallel to wb
 
-  // W given as a row-major [N][K] fp32 matrix → fragment order [N/16][K/32][64][8] bf16.
+  // W given as a row-major [N][K] fp32 matrix → fragment order [N/16][K/32][64][8] bf16 (and, with
+  // `wlo`, the residuals bf16(w − hi) in the same order).
   GemmDesc gemm(const std::vector<float>& w, int N, int K, const float* bias, const float* scale) {
     GemmDesc d{};
     const int Np = r16(N), Kp = r32(K);
@@ -340,8 +374,36 @@ struct Packer {
         for (int lane = 0; lane < 64; ++lane)
           for (int j = 0; j < 8; ++j) {
             const int n = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
-            wb.push_back(n < N && k < K ? f2bf(w[(size_t)n * K + k]) : 0);
+            const float x = n < N && k < K ? w[(size_t)n * K + k] : 0.f;
+            const uint16_t h = f2bf(x);
+            wb.push_back(h);
+            if (wlo) wlo->push_back(f2bf(x - bf2f(h)));
           }
+    d.bias = bias ? vec(bias, N, Np) : NONE;
+    d.scale = scale ? vec(scale, N, Np) : NONE;
+    return d;
+  }
+  // An LSQ integer grid q ∈ [−128, 127] as e4m3 pairs (v4 P_FP8): lane fragment = 8 bytes of
+  // 16·⌊q/16⌋ then 8 bytes of q mod 16, both exact in e4m3; same 16 B per lane per k-step as bf16.
+  GemmDesc gemm_fp8(const std::vector<float>& q, int N, int K, const float* bias, const float* scale) {
+    GemmDesc d{};
+    const int Np = r16(N), Kp = r32(K);
+    d.w = (uint32_t)(wb.size() / 8);
+    d.n = (uint16_t)Np;
+    d.k = (uint16_t)Kp;
+    for (int nt = 0; nt < Np / 16; ++nt)
+      for (int ks = 0; ks < Kp / 32; ++ks)
+        for (int lane = 0; lane < 64; ++lane) {
+          uint8_t by[16];
+          for (int j = 0; j < 8; ++j) {
+            const int n = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
+            const int v = n < N && k < K ? (int)q[(size_t)n * K + k] : 0;
+            const int hi = (int)std::floor(v / 16.0);
+            by[j] = f2e4m3((float)(16 * hi));
+            by[8 + j] = f2e4m3((float)(v - 16 * hi));
+          }
+          for (int j = 0; j < 8; ++j) wb.push_back((uint16_t)(by[2 * j] | (by[2 * j + 1] << 8)));
+        }
     d.bias = bias ? vec(bias, N, Np) : NONE;
     d.scale = scale ? vec(scale, N, Np) : NONE;
     return d;
@@ -376,6 +438,46 @@ float lsq_grid(std::vector<float>& w, float s, int bits) {
   return qmax;
 }
 
+// Largest |q| of every LSQ integer grid the engine would pack (0 without LSQ).
+float lsq_qmax(cet_engine* e) {
+  float qmax = 0.f;
+  if (e->icfg.lsq_bits <= 0) return qmax;
+  for (const auto& kv : e->weights) {
+    const std::string& n = kv.first;
+    const std::string suf = ".step_size";
+    if (n.size() <= suf.size() || n.compare(n.size() - suf.size(), suf.size(), suf) != 0 || !kv.second.loaded)
+      continue;
+    const std::string wn = n.substr(0, n.size() - suf.size()) + ".weight";
+    if (!e->has(wn)) continue;
+    std::vector<float> w = e->W(wn);
+    qmax = std::max(qmax, lsq_grid(w, e->scalar(n), e->icfg.lsq_bits));
+  }
+  return qmax;
+}
+
+// The v4 operand precision (cet_v4.hpp): the requested one, or automatically split bf16 where
+// bf16 cannot carry the model — an LSQ grid with |q| > 256, or a genuinely sparse masked decoder
+// (u < L_dec), whose unselected rows take cumsum(V) so that a near-tie flip of the top-u selection
+// moves the output by O(1): there the sparsity measure must be as exact as the reference's.
+int resolve_precision(cet_engine* e, float qmax, int* out) {
+  const auto& c = e->icfg;
+  const int Ld = c.label_len + c.out_len;
+  const bool sparse_dec = c.attn_prob && u_part(c.factor, Ld) < Ld;
+  int P = e->prec_req;
+  if (P < 0) P = (e->variant == 4 && (qmax > 256.f || sparse_dec)) ? 1 : 0;
+  if (P == 2) {
+    if (c.lsq_bits <= 0 || c.lsq_bits > 8)
+      return fail(CET_E_INVALID, "fp8 activations need an LSQ engine of at most 8 bits (integer grid in e4m3 pairs)");
+    if (qmax > 128.f) return fail(CET_E_INVALID, "fp8 weight pairs hold |q| <= 128");
+  }
+  if (P == 0 && qmax > 256.f)
+    return fail(CET_E_INVALID, "LSQ grid with |q| = " + std::to_string((int)qmax) +
+                                   " > 256 is not exact in bf16; use the split-bf16 precision");
+  if (P != 0 && e->variant != 4) return fail(CET_E_INVALID, "precision modes need the v4 kernel");
+  *out = P;
+  return CET_OK;
+}
+
 int build_informer(cet_engine* e) {
   const auto& c = e->icfg;
   const int D = c.d_model;
@@ -383,12 +485,21 @@ int build_informer(cet_engine* e) {
   auto& pb = e->pblob;
   wb.clear();
   pb.clear();
+  e->wblob_lo.clear();
   Packer pk{wb, pb};
   InformerPlan& p = e->ip;
   std::memset(&p, 0, sizeof(p));
   const bool lsq = c.lsq_bits > 0;
   const int bits = c.lsq_bits;
   float qmax = 0.f;   // largest |q| of the LSQ integer grids
+  int P = 0;
+  {
+    const int rc = resolve_precision(e, lsq_qmax(e), &P);
+    if (rc) return rc;
+  }
+  e->prec = P;
+  p.prec = P;
+  if (P == 1) pk.wlo = &e->wblob_lo;
 
   auto lin = [&](const std::string& n) { return e->W(n + ".weight"); };
   // Linear/conv1x1 (possibly several concatenated along the output axis) → GemmDesc
@@ -409,6 +520,7 @@ int build_informer(cet_engine* e) {
     }
     (void)conv1x1;
     const int N = (int)w.size() / K;
+    if (P == 2) return pk.gemm_fp8(w, N, K, b.data(), s.data());
     return pk.gemm(w, N, K, b.data(), lsq ? s.data() : nullptr);
   };
 
@@ -519,7 +631,7 @@ int build_informer(cet_engine* e) {
           sc[n] = (float)(inv * step);
           sh[n] = (float)(((double)cb[n] - rm[n]) * inv + bb[n]);
         }
-        d.conv = pk.gemm(m, D, 3 * D, sh.data(), sc.data());
+        d.conv = P == 2 ? pk.gemm_fp8(m, D, 3 * D, sh.data(), sc.data()) : pk.gemm(m, D, 3 * D, sh.data(), sc.data());
         d.L_out = (L - 1) / 2 + 1;
         d.dbg_conv = (int)dbg;
         jstage("enc" + std::to_string(i) + "_conv" + std::to_string(l), dbg, d.L_out, D);
@@ -539,9 +651,7 @@ int build_informer(cet_engine* e) {
     dbg += (int64_t)L * D;
   }
   p.S = S;
-  if (qmax > 256.f)
-    return fail(CET_E_INVALID, "LSQ grid with |q| = " + std::to_string((int)qmax) +
-                                   " > 256 is not exact in bf16 (step sizes too small for the bit width)");
+  (void)qmax;
   const int Ld = c.label_len + c.out_len;
   p.dbg_dec_emb = (int)dbg;
   jstage("dec_emb", dbg, Ld, D);
@@ -656,6 +766,30 @@ int build_informer(cet_engine* e) {
     p.lds3_ENC = V3L_ENC;
   }
   p.lds3_bytes = al(p.lds3_ENC + SP * BS * 2);
+  // v4: fixed regions (cet_plan.hpp v4_*) | stack output | [x_dec staged at entry, when two sequences
+  // per CU still fit with it: its HBM latency then overlaps the LDS zeroing; else it is requested
+  // before the last encoder norm, into CTX] | [sampler state: in-kernel replay path only]
+  {
+    const int RS = v4_rs(P), planes = v4_planes(P);
+    p.lds4_cnt = v4_cnt(P);
+    p.lds4_enc = v4_enc(P);
+    p.lds4_enc_lo = SP * RS;
+    p.lds4_zero = al(p.lds4_enc + planes * SP * RS);
+    p.lds4_bytes = p.lds4_zero;
+    p.lds4_xdec = -1;
+    const int xdec_bytes = al(Ld * p.in_stride * 4);
+    if (p.lds4_bytes + xdec_bytes <= V3_LDS_2PERCU || P == 1) {
+      p.lds4_xdec = p.lds4_bytes;
+      p.lds4_bytes += xdec_bytes;
+    }
+    p.lds4_lab = p.lds4_bytes;
+    p.lds4_bytes = al(p.lds4_bytes + c.out_len * c.c_out * 4);
+    p.lds4_mt = p.lds4_bytes;
+    p.lds4_bytes_replay = al(p.lds4_mt + MT_WORDS_HOST * 4);
+    if (LMAX * p.in_stride * 4 > v4_ctx_bytes(P) || Ld > 48 || p.lds4_bytes_replay > 160 * 1024)
+      return fail(CET_E_INVALID, "v4 LDS layout: staged input, decoder length or LDS size out of range");
+  }
+  p.stack = c.stack;
   return CET_OK;
 }
 
@@ -697,7 +831,8 @@ int upload(cet_engine* e) {
   if (!e->d_plan) HIP_TRY(hipMalloc(&e->d_plan, sizeof(InformerPlan) > sizeof(TransformerPlan)
                                                   ? sizeof(InformerPlan) : sizeof(TransformerPlan)));
   HIP_TRY(hipMemcpy(e->d_plan, plan, plan_bytes, hipMemcpyHostToDevice));
-  const size_t wbytes = e->wblob.size() * 2, pbytes = e->pblob.size() * 4;
+  const size_t hbytes = e->wblob.size() * 2, lbytes = e->wblob_lo.size() * 2;
+  const size_t wbytes = hbytes + lbytes, pbytes = e->pblob.size() * 4;
   if (wbytes > e->d_w_bytes) {
     if (e->d_w) HIP_TRY(hipFree(e->d_w));
     HIP_TRY(hipMalloc(&e->d_w, wbytes));
@@ -708,7 +843,8 @@ int upload(cet_engine* e) {
     HIP_TRY(hipMalloc((void**)&e->d_p, pbytes + 64));
     e->d_p_bytes = pbytes;
   }
-  HIP_TRY(hipMemcpy(e->d_w, e->wblob.data(), wbytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_w, e->wblob.data(), hbytes, hipMemcpyHostToDevice));
+  if (lbytes) HIP_TRY(hipMemcpy((char*)e->d_w + hbytes, e->wblob_lo.data(), lbytes, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_p, e->pblob.data(), pbytes, hipMemcpyHostToDevice));
   if (e->kind == 0) {
     for (int i = 0; i < cet_engine::NSLOT; ++i) {
@@ -913,7 +1049,7 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   e->kind = 0;
   e->icfg = *cfg;
   if (const char* v = std::getenv("CET_KERNEL"))
-    e->variant = std::strcmp(v, "v1") == 0 ? 1 : 3;
+    e->variant = std::strcmp(v, "v1") == 0 ? 1 : (std::strcmp(v, "v3") == 0 ? 3 : 4);
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
   const auto& c = *cfg;
@@ -1087,12 +1223,33 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   const InformerPlan& p = e->ip;
   switch (e->variant) {
     case 1: return cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
+    case 4: {
+      InformerArgs b = a;
+      b.wlo = (uint32_t)(e->wblob.size() * 2);
+      const bool replay = a.mt_in && !a.cnt;
+      return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);
+    }
     default: return cet_launch_informer_v3(&a, e->icfg.d_ff, p.lds3_bytes, p.lds3_XDEC >= 0, st);
   }
 }
 
+static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
+                        const float* label, float* nmse_acc, double* nmse_sums, void* stream);
+
 int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
                 void* stream) {
+  return forward_impl(e, x_enc, x_dec, B, out, attns, nullptr, nullptr, nullptr, stream);
+}
+
+int cet_forward_nmse(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, const float* label,
+                     float* nmse_acc, double* nmse_sums, void* stream) {
+  if (!label || (!nmse_acc && !nmse_sums)) return fail(CET_E_INVALID, "null argument");
+  if (e && e->kind != 0) return fail(CET_E_INVALID, "cet_forward_nmse: Informer engines only");
+  return forward_impl(e, x_enc, x_dec, B, out, nullptr, label, nmse_acc, nmse_sums, stream);
+}
+
+static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
+                        const float* label, float* nmse_acc, double* nmse_sums, void* stream) {
   if (!e || !x_enc || !x_dec || !out) return fail(CET_E_INVALID, "null argument");
   if (B < 0 || B > (1 << 24)) return fail(CET_E_INVALID, "bad batch size");
   int rc = finalize(e);
@@ -1132,6 +1289,35 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   a.dbg = e->dbg;
   a.stamps = e->stamps;
   a.B = B;
+  a.wlo = 0;
+  a.lds_bytes = 0;
+  a.label = nullptr;
+  a.nmse_part = nullptr;
+  a.nmse_acc = nullptr;
+  a.nmse_sums = nullptr;
+  // NMSE_Split of this forward's output: fused into the v4 kernel's epilogue (one n-tile of outputs),
+  // else the standalone reduction right after the forward on the same stream
+  const bool fuse_nmse = label && e->variant == 4 && e->icfg.c_out <= 16;
+  if (fuse_nmse) {
+    const size_t need = (size_t)B * e->icfg.out_len;
+    if (need > e->nmse_part_n) {
+      if (e->d_nmse_part) HIP_TRY(hipFree(e->d_nmse_part));
+      HIP_TRY(hipMalloc((void**)&e->d_nmse_part, need * sizeof(float2)));
+      e->nmse_part_n = need;
+    }
+    a.label = label;
+    a.nmse_part = e->d_nmse_part;
+    a.nmse_acc = nmse_acc;
+    a.nmse_sums = nmse_sums;
+    a.ticket = e->d_ticket;
+  }
+  auto finish_nmse = [&]() -> int {
+    if (!label || fuse_nmse) return CET_OK;
+    if (cet_launch_nmse_split(out, label, B, e->icfg.out_len, e->icfg.c_out, nmse_acc, nullptr, 1, nmse_sums,
+                              (hipStream_t)stream))
+      return fail(CET_E_HIP, "nmse launch failed");
+    return CET_OK;
+  };
   // explicit indices (cet_set_prob_indices for every call) win for this one forward
   bool explicit_idx = p.n_calls > 0, any_idx = false;
   for (int c = 0; c < p.n_calls; ++c) {
@@ -1154,7 +1340,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
       e->dev_mt_valid = true;
       e->tab_ready = false;
     }
-    const bool prep = e->variant == 3 && B >= cet_engine::PREP_MIN_B;
+    const bool prep = e->variant >= 3 && B >= cet_engine::PREP_MIN_B;
     if (prep && !e->tab_ready) {
       // first forward after a (re)seed: this forward's tables from a one-workgroup launch
       const int lds = std::max(640 * 4 + (p.lds3_MT - p.lds3_CNT), std::min(replay_fast_lds(p), 64 * 1024));
@@ -1172,7 +1358,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
         a.mt_in = e->d_mt + 640 * e->mt_cur;
         a.mt_out = e->d_mt + 640 * (1 - e->mt_cur);
         a.cnt_next = e->d_tab[1 - e->tab_cur];
-        a.ticket = e->d_ticket;
+        a.ticket = e->d_ticket;   // (also the fused NMSE's finish counter)
         e->mt_cur = 1 - e->mt_cur;
         e->tab_cur = 1 - e->tab_cur;
       } else {
@@ -1188,7 +1374,7 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
     rc = launch_fused(e, a, st);
     if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
     if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
-    return CET_OK;
+    return finish_nmse();
   }
   // ---- this forward's ProbSparse draws → key multiplicity tables (host-built)
   const bool native_now = e->native_rng && !explicit_idx;
@@ -1232,13 +1418,30 @@ int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, fl
   rc = launch_fused(e, a, st);
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   if (rc) return fail(CET_E_HIP, std::string("informer launch failed: ") + hipGetErrorString(hipGetLastError()));
-  return CET_OK;
+  return finish_nmse();
 }
 
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   e->stamps = reinterpret_cast<unsigned long long*>(stamps_dev);
   return CET_OK;
+}
+
+int cet_set_precision(cet_engine* e, int prec) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (e->kind != 0) return fail(CET_E_INVALID, "precision modes are Informer-engine only");
+  if (prec < -1 || prec > 2) return fail(CET_E_INVALID, "precision must be -1 (auto), 0 (bf16), 1 (split bf16) or 2 (fp8)");
+  e->prec_req = prec;
+  e->dirty = true;
+  return CET_OK;
+}
+
+int cet_get_precision(cet_engine* e) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (e->kind != 0) return 0;
+  const int rc = finalize_host(e);
+  if (rc) return rc;
+  return e->prec;
 }
 
 int cet_set_sampler(cet_engine* e, int on_host) {
@@ -1250,7 +1453,8 @@ int cet_set_sampler(cet_engine* e, int on_host) {
 
 int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
-  if (variant != 1 && variant != 3) return fail(CET_E_INVALID, "variant must be 1 or 3");
+  if (variant != 1 && variant != 3 && variant != 4) return fail(CET_E_INVALID, "variant must be 1, 3 or 4");
+  if (variant != e->variant) e->dirty = true;   // the precision resolution depends on the kernel
   if (e->kind != 0 && variant != 1) return fail(CET_E_INVALID, "the Transformer engine has one variant");
   e->variant = variant;
   return CET_OK;

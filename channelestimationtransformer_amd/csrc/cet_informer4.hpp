@@ -1,0 +1,458 @@
+// Fused InformerStack forward, v4: the v3 structure (512-thread workgroups, one residual n-tile and
+// one attention head per wave, two sequences per CU) with the operand precision as a template
+// policy (cet_v4.hpp) and a plan-sized LDS layout.  Instantiated per precision in
+// cet_informer4_{bf16,x3,fp8}.hip (parallel builds).
+//
+// Reference: FullPrecision/InformerModel/model.py:142-271 (InformerStack), :11-139 (Informer),
+// encoder.py:6-106, decoder.py:6-56, attn.py:37-209, embed.py:8-135; models/InformerLSQ/LSQ.py:65-74,
+// 305-314 (LSQ weight grid, P_FP8 / P_X3 carriers).
+#pragma once
+#include "cet_kernels.h"
+#include "cet_mt.hpp"
+#include "cet_sampler.hpp"
+#include "cet_v4.hpp"
+
+namespace cet {
+namespace v4 {
+
+template <int N>
+using IC = std::integral_constant<int, N>;
+
+__device__ __forceinline__ void stage(const float* __restrict__ src, float* dst, int L, int C, int CS) {
+  for (int i = threadIdx.x; i < L * C; i += NTHREADS) {
+    const int t = i / C, c = i - t * C;
+    dst[t * CS + c] = src[i];
+  }
+}
+
+// Plan access point: read through the constant address space behind an opaque pointer, so each
+// phase re-loads its descriptors with scalar loads instead of keeping them live in SGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
+#else
+template <class T>
+using cptr = const T*;
+#endif
+template <class T>
+__device__ __forceinline__ cptr<T> fresh(const T* p) {
+  cptr<T> c = (cptr<T>)p;
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
+__device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
+  if (d.bias != NONE) d.bias += off;
+  if (d.scale != NONE) d.scale += off;
+  return d;
+}
+
+// P: precision of the dense (LSQ-quantisable) layers; DIAG: the instance that honours the optional
+// outputs (attns maps, activation dumps, phase stamps) — the production instance compiles them out.
+template <int DFF, bool DIAG, int P>
+__device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+#define PL (*fresh(plan))
+#define ELD (PL.enc[first + l])
+#define DLD (PL.dec[l])
+  constexpr int PP = plain_of<P>();       // embedding / projection precision
+  using G = Geo<P>;
+  const Mem M{make_rsrc(a.weights), make_rsrc(a.params), a.wlo};
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  const int w = wave_id();
+
+  const Img<P> XB{lds + V4L_XB, G::IMG};
+  const Img<P> CTXI{lds + v4_ctx(P), G::IMG};                           // attention context / FFN hidden
+  const Img<P> ENC{lds + v4_enc(P), PL.lds4_enc_lo};                    // encoder-stack output
+  const Img<PP> FIN{lds + v4_ctx(P), Geo<PP>::IMG};                      // decoder output (projection input)
+  float* LNP = reinterpret_cast<float*>(lds + v4_scr(P));            // LN partials (alias the scratch)
+  uint8_t* CNT = reinterpret_cast<uint8_t*>(lds + v4_cnt(P));
+  MTState gen{reinterpret_cast<uint32_t*>(lds + PL.lds4_mt), MT_N};
+  float* SCR = reinterpret_cast<float*>(lds + v4_scr(P)) + w * SCR_FLOATS;
+  float* IN = reinterpret_cast<float*>(lds + v4_ctx(P));                // staged raw input (aliases CTX)
+  float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
+
+  if (DIAG && a.stamps && threadIdx.x == 0) a.stamps[(size_t)b * MAX_STAMPS + 127] = __builtin_amdgcn_s_memtime();
+  const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride, Ld = PL.dec_len;
+  // this sequence's x_enc rows are requested first (one f32x4 per thread: L·C/4 ≤ 384), so their HBM
+  // latency overlaps the LDS zeroing
+  const int t4 = 4 * (int)threadIdx.x;
+  const int xdec_off = PL.lds4_xdec;   // x_dec's own region (staged now) or -1 (staged before the decoder)
+  float* XDEC = reinterpret_cast<float*>(lds + (xdec_off >= 0 ? xdec_off : v4_ctx(P)));
+  f32x4 xe4 = {0.f, 0.f, 0.f, 0.f}, xd4 = xe4;
+  if (t4 < L0 * C) xe4 = *reinterpret_cast<const f32x4*>(a.x_enc + (size_t)b * L0 * C + t4);
+  if (xdec_off >= 0 && t4 < Ld * C) xd4 = *reinterpret_cast<const f32x4*>(a.x_dec + (size_t)b * Ld * C + t4);
+  // fused NMSE: this sequence's labels (pred_len × c_out, c_out ≤ 16) staged with the inputs
+  float* LAB = reinterpret_cast<float*>(lds + PL.lds4_lab);
+  const int nlab = PL.pred_len * PL.c_out;
+  f32x4 lb4 = {0.f, 0.f, 0.f, 0.f};
+  if (a.label && t4 < nlab) lb4 = *reinterpret_cast<const f32x4*>(a.label + (size_t)b * nlab + t4);
+  // zero the activation images: rows past L are read (never used) by MFMAs
+  for (int i = threadIdx.x; i < PL.lds4_zero / 16; i += NTHREADS)
+    reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();   // zeroing done before the staged rows land in CTX
+  if (t4 < L0 * C) *reinterpret_cast<f32x4*>(IN + (t4 >> PL.C_shift) * CS + (t4 & (C - 1))) = xe4;
+  if (xdec_off >= 0 && t4 < Ld * C) *reinterpret_cast<f32x4*>(XDEC + (t4 >> PL.C_shift) * CS + (t4 & (C - 1))) = xd4;
+  if (a.label && t4 < nlab) *reinterpret_cast<f32x4*>(LAB + t4) = lb4;
+
+  Res<MT> X;
+  unsigned long long* stamps = DIAG && a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
+  int sid = 0;
+  auto STAMP = [&]() {
+    if (stamps) {
+      if (threadIdx.x == 0 && sid < MAX_STAMPS) stamps[sid] = __builtin_amdgcn_s_memtime();
+      ++sid;
+    }
+  };
+  if (a.mt_in && !a.cnt) {
+    __syncthreads();
+    mt_load<NTHREADS>(gen, a.mt_in);
+  }   // device-resident sampler (cet_mt.hpp)
+  auto FINE = [&](int layer, int k) {
+    if (stamps && layer == 0 && threadIdx.x == 0) stamps[116 + k] = __builtin_amdgcn_s_memtime();
+  };
+  STAMP();
+
+  constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // 16-byte lane fragments per n-tile at K = 128
+  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles
+  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
+                    uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
+                    int mix, int call, float* attn_out) {
+    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    HeadIO<P> io;
+    io.xq = Xq; io.xkv = Xkv; io.ctx = CTXI; io.wq = Wq; io.wk = Wk; io.wv = Wv;
+    io.dq = dq; io.dk = dk; io.dv = dv;
+    io.LQ = LQ; io.LK = LK; io.prob = prob; io.causal = causal; io.mix = mix; io.u = LQ;
+    io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = attn_out; io.m_dbg = nullptr;
+    io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
+    if (call >= 0) {
+      const AttnCall& c = PL.calls[call];
+      io.u = c.u;
+      io.cnt_stride = c.cnt_stride;
+      if (dbg && c.m_dbg >= 0) io.m_dbg = dbg + c.m_dbg;
+      const bool sparse = c.u < c.LQ;
+      if (!a.cnt) {
+        // resident sampler: replay this call's draws into the LDS table (cet_mt.hpp)
+        mt_replay<NTHREADS>(gen, c.LQ, c.U, c.LK, sparse ? reinterpret_cast<uint32_t*>(CNT) : nullptr,
+                            c.cnt_stride);
+        if (call == PL.n_calls - 1 && b == 0) mt_store<NTHREADS>(gen, a.mt_out);
+      } else if (sparse) {
+        const int bytes = ((c.LQ + 15) & ~15) * c.cnt_stride;
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + c.cnt_off);
+        f32x4* dst = reinterpret_cast<f32x4*>(CNT);
+        for (int i = threadIdx.x; i < bytes / 16; i += NTHREADS) dst[i] = src[i];
+        __syncthreads();
+      }
+      if (sparse) io.cnt = CNT;
+    }
+    attention_head<P, MQ_, MK_>(io, M, w);
+  };
+
+  for (int e = 0; e < PL.n_enc; ++e) {
+    if (e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);   // CTX was reused by encoder e-1
+    __syncthreads();
+    // ---- DataEmbedding (embed.py:132-135) on the EncoderStack window x[:, -L:] (encoder.py:95-106)
+    int L = L0 >> e;
+    const int off = L0 - L;
+    int nmt = (L + 15) >> 4;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) X.v[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      const GemmDesc d = PL.emb_enc;
+      gemm_res<PP, 2, MT>(M, d, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, off}, [&](int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_op() & 15);
+        const int prow = m + off < LMAX ? m + off : LMAX - 1;
+        X.v[mt] = y + pload4(M, PL.pe_enc, prow * DMODEL + n0);
+      });
+    }
+    __syncthreads();                       // IN (aliases CTX) fully read
+    store_res(X, nmt, L, XB);
+    __syncthreads();
+    if (dbg && e == 0) dump_res(X, nmt, L, dbg + PL.dbg_emb);
+    STAMP();  // embedding
+
+    const int first = PL.enc_first[e];
+    for (int l = 0; l < PL.enc_layers[e]; ++l) {
+      L = ELD.L_in;
+      nmt = (L + 15) >> 4;
+      // ---- AttentionLayer + ProbAttention / FullAttention, one head per wave, context → CTX
+      {
+        const GemmDesc q = ELD.qkv;
+        auto enc_attend = [&](auto NQ) __attribute__((always_inline)) {
+          attend(NQ, NQ, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
+                 part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
+                 DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
+        };
+        switch (nmt) {
+          case 1: enc_attend(IC<1>{}); break;
+          case 2: enc_attend(IC<2>{}); break;
+          case 3: enc_attend(IC<3>{}); break;
+          default: enc_attend(IC<MT>{}); break;
+        }
+      }
+      const WPre<P, 4> po = prefetch_res<P, 4>(M, ELD.o);   // x = x + new_x (encoder.py:49)
+      __syncthreads();
+      STAMP();  // encoder attention
+      gemm_res<P, 4, MT>(po, nmt, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
+      FINE(l, 0);
+      static_assert(DFF / 16 <= NW, "FFN hidden n-tiles: at most one per wave");
+      const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, ELD.f1, DFF / 16);   // conv1 (k=1) + activation
+      ln_res(X, nmt, L, M, ELD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      STAMP();  // out-projection + LN1
+      {
+        const int relu = PL.act_relu;
+        gemm_tiles1<P, 4>(pf1, DFF / 16, nmt, LoadImg<P>{XB}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
+          CTXI.st4(mt * 16 + (lane_op() & 15), n0, v);
+        });
+      }
+      FINE(l, 1);
+      const WPre<P, DFF / 32> pf2 = prefetch_res<P, DFF / 32>(M, ELD.f2);  // conv2 (k=1) + residual
+      __syncthreads();
+      FINE(l, 2);
+      gemm_res<P, DFF / 32, MT>(pf2, nmt, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
+      FINE(l, 3);
+      const int has_conv = ELD.conv.n;
+      const bool last_of_stack = e == PL.n_enc - 1 && l == PL.enc_layers[e] - 1;
+      ln_res(X, nmt, L, M, ELD.ln2, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      STAMP();  // FFN + LN2
+      if (dbg && ELD.dbg_layer >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_layer);
+      FINE(l, 4);
+      if (has_conv) {
+        // ---- ConvLayer (encoder.py:22-28): circular conv, BN(eval) folded, ELU, MaxPool(3,2,1)
+        const GemmDesc d = ELD.conv;
+        with_nmt(nmt, [&](auto NMT) __attribute__((always_inline)) {
+          constexpr int N_ = decltype(NMT)::value;
+          Res<N_> Cv;
+          const WPre<P, 4> pcv = prefetch_kouter<P, 12, 4>(M, d);
+          gemm_kouter_res<P, 12, 4, N_>(pcv, M, d, LoadCirc3<P>{XB, L},
+                                        [&](int mt, int n0, f32x4 v) __attribute__((always_inline)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
+            Cv.v[mt] = v;
+          });
+          FINE(l, 5);
+          maxpool_res<N_>(Cv, L, X);
+        });
+        FINE(l, 6);
+        L = ELD.L_out;
+        nmt = (L + 15) >> 4;
+        __syncthreads();                   // every wave finished reading XB
+        FINE(l, 7);
+        store_res(X, nmt, L, XB);
+        __syncthreads();
+        STAMP();  // distil conv + pool
+        if (dbg && ELD.dbg_conv >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_conv);
+      }
+      (void)last_of_stack;
+    }
+    // ---- Encoder.norm (encoder.py:83-84) → this encoder's rows of the stack output (ENC)
+    const int rows = PL.enc_rows[e];
+    const Img<P> encw{ENC.base + PL.enc_row_off[e] * G::RS, ENC.lo};
+    ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, XB, &encw);
+    __syncthreads();
+    if (dbg && PL.enc_dbg[e] >= 0) dump_res(X, nmt, rows, dbg + PL.enc_dbg[e]);
+    STAMP();  // encoder norm
+  }
+
+  // ================================ decoder (decoder.py:43-56), instantiated for its compile-time
+  // tile count (dec_len ≤ 48); the staged decoder input is in XDEC
+  const int S = PL.S;
+  if (xdec_off < 0) {   // no room to keep it since entry: stage it now (into CTX, free after the encoder)
+    stage(a.x_dec + (size_t)b * Ld * C, XDEC, Ld, C, CS);
+    __syncthreads();
+  }
+  auto decoder = [&](auto NMDc, auto NMSc) __attribute__((always_inline)) {
+    constexpr int NMS = decltype(NMSc)::value;
+    constexpr int NMD = decltype(NMDc)::value;
+    const int nmd = NMD;
+    Res<NMD> XD;
+    {
+      const GemmDesc d = PL.emb_dec;
+      gemm_res_n<PP, 2, NMD>(M, d, LoadEmbed<PP>{XDEC, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_op() & 15);
+        const int prow = m < LMAX ? m : LMAX - 1;
+        XD.v[mt] = y + pload4(M, PL.pe_dec, prow * DMODEL + n0);
+      });
+    }
+    __syncthreads();
+    store_res(XD, nmd, Ld, XB);
+    __syncthreads();
+    if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_emb);
+    STAMP();  // decoder embedding
+
+    for (int l = 0; l < PL.d_layers; ++l) {
+      {
+        // masked self-attention with the mix scramble (model.py:211-222)
+        const GemmDesc q = DLD.qkv;
+        attend(IC<NMD>{}, IC<NMD>{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+               part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld, PL.prob, 1, PL.mix, DLD.call, nullptr);
+      }
+      const WPre<P, 4> po = prefetch_res<P, 4>(M, DLD.o);
+      __syncthreads();
+      STAMP();  // decoder self-attention
+      gemm_res_n<P, 4, NMD>(po, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      ln_res(XD, nmd, Ld, M, DLD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      {
+        // cross-attention: FullAttention over the encoder-stack output, mix=False
+        const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
+        attend(IC<NMD>{}, IC<NMS>{}, XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+               part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
+      }
+      const WPre<P, 4> pco = prefetch_res<P, 4>(M, DLD.co);
+      __syncthreads();
+      STAMP();  // cross-attention
+      gemm_res_n<P, 4, NMD>(pco, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, DLD.f1, DFF / 16);
+      ln_res(XD, nmd, Ld, M, DLD.ln2, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      {
+        const int relu = PL.act_relu;
+        gemm_tiles1<P, 4>(pf1, DFF / 16, nmd, LoadImg<P>{XB}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
+          CTXI.st4(mt * 16 + (lane_op() & 15), n0, v);
+        });
+      }
+      const WPre<P, DFF / 32> pf2 = prefetch_res<P, DFF / 32>(M, DLD.f2);
+      __syncthreads();
+      gemm_res_n<P, DFF / 32, NMD>(pf2, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      ln_res(XD, nmd, Ld, M, DLD.ln3, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3
+      if (dbg && DLD.dbg >= 0) dump_res(XD, nmd, Ld, dbg + DLD.dbg);
+    }
+    // final norm → the projection's input image (plain precision; CTX is free: FFN2 is done)
+    ln_res(XD, nmd, Ld, M, PL.dec_norm, 1e-5f, false, LNP, FIN, (const Img<PP>*)nullptr);
+    __syncthreads();
+    if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_out);
+    {
+      // projection (model.py:264) on the last pred_len rows → out[b]
+      const GemmDesc d = PL.proj;
+      const int first_row = Ld - PL.pred_len, co = PL.c_out;
+      float* out = a.out + (size_t)b * PL.pred_len * co;
+      const bool fuse = a.label != nullptr;   // the launcher guarantees c_out ≤ 16 (one n-tile)
+      gemm_tiles<PP, 4>(M, d, d.n / 16, nmd, LoadImg<PP>{FIN}, [&](int mt, int n0, f32x4 v) {
+        const int lane = lane_op();
+        const int m = mt * 16 + (lane & 15);
+        const bool valid = m >= first_row && m < Ld;
+        float se = 0.f, pw = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (valid && n0 + r < co) {
+            out[(m - first_row) * co + n0 + r] = v[r];
+            if (fuse) {   // NMSE_Split_cuda(x_hat = out, x = label): Σ(x − x̂)², Σ x̂² (metrics.py:26-30)
+              const float dx = LAB[(m - first_row) * co + n0 + r] - v[r];
+              se = fmaf(dx, dx, se);
+              pw = fmaf(v[r], v[r], pw);
+            }
+          }
+        if (fuse) {
+          se = xor_sum(se, 16);   // over the 16 features of row m (4 lane groups)
+          se = xor_sum(se, 32);
+          pw = xor_sum(pw, 16);
+          pw = xor_sum(pw, 32);
+          if ((lane >> 4) == 0 && valid) {
+            // write-through (sc1) so the last workgroup to finish reads it without a fence
+            const float2 pr = make_float2(se, pw);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.nmse_part + (size_t)b * PL.pred_len +
+                                                                     (m - first_row)),
+                               __builtin_bit_cast(unsigned long long, pr), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      });
+      if (fuse) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done
+    }
+    STAMP();  // final norm + projection
+  };
+  switch ((Ld + 15) >> 4) {
+    case 1: S <= 16 ? decoder(IC<1>{}, IC<1>{}) : decoder(IC<1>{}, IC<MT>{}); break;
+    case 2: S <= 16 ? decoder(IC<2>{}, IC<1>{}) : decoder(IC<2>{}, IC<MT>{}); break;
+    default: S <= 16 ? decoder(IC<3>{}, IC<1>{}) : decoder(IC<3>{}, IC<MT>{}); break;
+  }
+  // ---- the first workgroup to finish prepares the NEXT forward's ProbSparse tables from the
+  //      resident sampler state (cet_sampler.hpp) while the rest of the grid drains; the last one to
+  //      finish re-arms the counter for the next launch
+  if (a.ticket) {
+    __syncthreads();   // every wave's NMSE partials are written (each waited for its own stores)
+    unsigned* tk = reinterpret_cast<unsigned*>(lds + v4_scr(P));
+    unsigned tw = 0;
+    if (w == 0) {
+      if (threadIdx.x == 0) tw = atomicAdd(a.ticket, 1u);   // agent-scope add, value returned
+      tw = __shfl(tw, 0, 64);
+      if (threadIdx.x == 0) *tk = tw;
+      if (tw + 1u == (unsigned)a.B) {
+        // ---- last workgroup: the batch's NMSE_Split from every sequence's partials, summed in a fixed
+        //      order (lane l takes sequences l, l+64, ...; then a fixed butterfly): deterministic
+        if (a.label) {
+          const int T = PL.pred_len, lane = threadIdx.x & 63;
+          for (int t = 0; t < T; ++t) {
+            double se = 0.0, pw = 0.0;
+            for (int s = lane; s < a.B; s += 64) {
+              const unsigned long long u = __hip_atomic_load(
+                  reinterpret_cast<const unsigned long long*>(a.nmse_part + (size_t)s * T + t), __ATOMIC_RELAXED,
+                  __HIP_MEMORY_SCOPE_AGENT);
+              const float2 pr = __builtin_bit_cast(float2, u);
+              se += (double)pr.x;
+              pw += (double)pr.y;
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+              se += __shfl_xor(se, o, 64);
+              pw += __shfl_xor(pw, o, 64);
+            }
+            if (lane == 0) {
+              if (a.nmse_sums) {
+                a.nmse_sums[t] = se;
+                a.nmse_sums[T + t] = pw;
+              }
+              if (a.nmse_acc) a.nmse_acc[t] += (float)(se / pw);
+            }
+          }
+        }
+        if (threadIdx.x == 0) atomicExch(a.ticket, 0u);   // re-arm for the next launch
+      }
+    }
+    __syncthreads();
+    const bool elected = __builtin_amdgcn_readfirstlane(*tk) == 0u;
+    __syncthreads();   // every wave has read the ticket before the replay reuses the LDS
+    if (elected && a.cnt_next)
+      replay_all<NTHREADS>(PL, a.mt_in, a.mt_out, a.cnt_next, lds, a.lds_bytes, reinterpret_cast<uint32_t*>(lds),
+                           reinterpret_cast<uint32_t*>(lds + v4_ctx(P)));
+  }
+#undef PL
+#undef ELD
+#undef DLD
+}
+
+// X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
+template <int DFF, bool DIAG, int P>
+__global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
+    informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
+  informer_forward_v4_body<DFF, DIAG, P>(a, plan);
+}
+
+template <int P>
+int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
+  if (a->B <= 0) return 0;
+  const bool diag = a->attns || a->dbg || a->stamps;
+  using K = void (*)(InformerArgs, const InformerPlan*);
+  K kern = nullptr;
+  if (dff == 64) kern = diag ? informer_forward_v4<64, true, P> : informer_forward_v4<64, false, P>;
+  else if (dff == 128) kern = diag ? informer_forward_v4<128, true, P> : informer_forward_v4<128, false, P>;
+  else return -3;
+  if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
+  InformerArgs args = *a;
+  args.lds_bytes = lds_bytes;
+  hipLaunchKernelGGL(kern, dim3(a->B), dim3(NTHREADS), lds_bytes, stream, args, a->plan);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace v4
+}  // namespace cet

@@ -1,0 +1,7 @@
+// v4 fused Informer instances for the P_FP8 operand policy (cet_informer4.hpp; one precision per
+// translation unit so the instances compile in parallel).
+#include "cet_informer4.hpp"
+
+extern "C" int cet_launch_informer_v4_p2(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
+  return cet::v4::launch_v4<cet::v4::P_FP8>(a, dff, lds_bytes, stream);
+}

@@ -25,6 +25,13 @@ struct InformerArgs {
   float* dbg;                 // optional per-stage activation dump
   unsigned long long* stamps; // optional per-phase s_memtime stamps [B][CET_MAX_STAMPS] (diagnostics)
   int B;
+  uint32_t wlo;               // v4 split-bf16: byte offset of the lo weight fragments in `weights`
+  int lds_bytes;              // dynamic LDS of the launch (set by the launcher)
+  // v4 fused NMSE_Split (FullPrecision/metrics.py:26-30) of (out, label) over the batch, or label = null
+  const float* label;         // [B][pred_len][c_out] (c_out ≤ 16)
+  float2* nmse_part;          // [B][pred_len] per-sequence (Σ(x−x̂)², Σx̂²), written write-through (sc1)
+  float* nmse_acc;            // [pred_len] ratio, accumulated (+=) by the last workgroup, or null
+  double* nmse_sums;          // [2][pred_len] global sums (overwritten) by the last workgroup, or null
 };
 
 // device channel pipeline (cet_data.hip)
@@ -76,6 +83,7 @@ extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint
                                        uint8_t* tab_out, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, int xdec_early,
                                       hipStream_t stream);
+extern "C" int cet_launch_informer_v4(const cet::InformerArgs* a, int prec, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);

@@ -94,6 +94,13 @@ struct InformerPlan {
   // v3 (8-wave) layout: the LayerNorm partials alias the per-wave attention scratch
   int lds3_XB, lds3_CTX, lds3_ENC, lds3_SCR, lds3_CNT, lds3_MT, lds3_bytes;
   int lds3_XDEC;            // staged decoder input (byte offset), or -1
+  // v4 layout (cet_plan.hpp v4_*): the fixed regions, the encoder-stack output (planes × S_pad rows),
+  // the staged x_dec and, for the in-kernel sampler replay, its state
+  int lds4_enc, lds4_enc_lo, lds4_cnt, lds4_mt, lds4_zero, lds4_bytes, lds4_bytes_replay;
+  int lds4_xdec;            // x_dec staged at kernel entry (byte offset), or -1: staged before the decoder
+  int lds4_lab;             // labels of the fused NMSE (pred_len × c_out fp32), staged at kernel entry
+  int prec;                 // v4 operand precision of the dense layers (v4::P_BF16 / P_X3 / P_FP8)
+  int stack;
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
   int draws;                // mt19937 words one forward consumes (Σ LQ·U over every call)
@@ -119,6 +126,32 @@ constexpr int V3_LDS_2PERCU = 80 * 1024;               // two sequences per CU
 // per CU with it (InformerPlan::lds3_XDEC = V3L_XDEC), else x_dec is staged into CTX when the
 // decoder starts (lds3_XDEC = -1).
 static_assert(V3L_CTX % 16 == 0 && V3L_SCR % 16 == 0 && V3L_CNT % 16 == 0 && V3L_ENC_XE % 16 == 0, "16-B regions");
+
+// v4 LDS layout (precision P: 0 bf16, 1 split-bf16 hi/lo planes, 2 fp8); every offset the kernel
+// uses in its phases is a compile-time constant (folded into ds_* immediates):
+//   image XB | context / FFN hidden / staged input / projection input (CTX) | per-wave attention
+//   scratch aliased by the LayerNorm partials | multiplicity table | stack output (plan-sized) |
+//   [x_dec staged at entry] | [sampler state, in-kernel replay only]
+// Image rows: bf16 272 B (v3's stride; 288 B — conflict-free ds_read_b128 — measured no faster), fp8
+// 144 B (conflict-free ds_read_b64).
+#ifndef V4_RS16
+#define V4_RS16 272   // A/B knob: bf16 image row stride (bytes); 288 (conflict-free ds_read_b128) measured equal
+#endif
+constexpr int v4_rs(int P) { return P == 2 ? 144 : V4_RS16; }
+constexpr int v4_planes(int P) { return P == 1 ? 2 : 1; }
+constexpr int v4_img(int P) { return LMAX * v4_rs(P); }
+constexpr int v4_max3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
+constexpr int V4L_XB = 0;
+constexpr int v4_ctx(int P) { return v4_planes(P) * v4_img(P); }
+constexpr int v4_ctx_bytes(int P) {
+  // context image | staged fp32 input rows (LMAX × 20 floats) | the bf16 projection input (48 rows)
+  return v4_max3(v4_planes(P) * v4_img(P), LMAX * 20 * 4, 48 * v4_rs(0) * v4_planes(P == 2 ? 0 : P));
+}
+constexpr int v4_scr(int P) { return v4_ctx(P) + v4_ctx_bytes(P); }
+constexpr int v4_cnt(int P) { return v4_scr(P) + 8 * V2_SCR_FLOATS * 4; }   // multiplicity table, LMAX rows
+constexpr int v4_enc(int P) { return v4_cnt(P) + LMAX * 96; }               // stack output (plan-sized)
+static_assert(LMAX * LN3_STRIDE * 4 <= 8 * V2_SCR_FLOATS * 4, "LN partials fit the scratch they alias");
+static_assert(v4_ctx(0) % 16 == 0 && v4_scr(0) % 16 == 0 && v4_enc(1) % 16 == 0 && v4_enc(2) % 16 == 0, "16-B");
 
 // LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded
 // mt19937 state | the forward's tempered words | every call's multiplicity table.

@@ -1,0 +1,905 @@
+// "v4" building blocks: the v3 scheme (8-wave workgroups, one 16-feature n-tile of the register
+// residual and one attention head per wave) with the operand precision as a compile-time policy:
+//
+//   P_BF16  bf16 operands, fp32 accumulation (the C2 contract).
+//   P_X3    split bf16: every operand x is carried as hi = bf16(x), lo = bf16(x − hi) and a product
+//           is hi·hi + hi·lo + lo·hi on three MFMAs (≈16 significant bits per operand, fp32
+//           accumulation): the fp32-parity mode, and the exact carrier of LSQ integer grids whose
+//           |q| exceeds bf16's 256.
+//   P_FP8   OCP e4m3 activations on v_mfma_f32_16x16x32_fp8_fp8 for the LSQ-quantised layers; the
+//           integer weight grid q ∈ [−128, 127] is carried exactly as 16·⌊q/16⌋ and q mod 16 (both
+//           e4m3-exact), two MFMAs per k-step; the step size sits in the epilogue.  The layers the
+//           reference does not quantise (token embedding, projection) and the attention products
+//           stay bf16.
+//
+// Fragment geometry is the same for every policy (v_mfma_f32_16x16x32_*: lane l holds A[row l&15]
+// [k = 8(l>>4) .. +7] and B[k = 8(l>>4) .. +7][col l&15]), so the GEMM loops are shared; only the
+// element type of a fragment, the number of MFMAs per k-step and the image format change.
+//
+// Images (LDS): bf16 rows of 288 B (18 16-byte slots: the 16 lanes of every ds_read_b128 lane group
+// hit 16 distinct slots — conflict-free, MI355X_MICROARCH §LDS), X3 adds a lo plane, fp8 rows are
+// 144 B (conflict-free ds_read_b64).
+#pragma once
+#include <type_traits>
+
+#include "cet_device.hpp"
+
+namespace cet {
+namespace v4 {
+
+enum { P_BF16 = 0, P_X3 = 1, P_FP8 = 2 };
+// precision of the layers the reference never quantises, and of the attention products
+template <int P>
+constexpr int plain_of() { return P == P_FP8 ? P_BF16 : P; }
+
+constexpr int NW = 8;
+constexpr int NTHREADS = NW * WAVE;
+constexpr int MT = 6;                 // max 16-row tiles (96 positions)
+constexpr int LN_STRIDE = LN3_STRIDE;
+constexpr int SCR_FLOATS = V2_SCR_FLOATS;   // per-wave attention scratch (u64 keys | int16 sel | flags)
+
+template <int P>
+struct Geo {
+  static constexpr int RS = v4_rs(P);                 // image row stride (bytes)
+  static constexpr int PLANES = P == P_X3 ? 2 : 1;
+  static constexpr int IMG = LMAX * RS;                // one plane of a LMAX-row image
+};
+
+// ------------------------------------------------------------------ fragments and products
+template <int P>
+struct XF {  // B-role (activation) fragment of one 16x16x32 k-step
+  bf16x8 h;
+};
+template <>
+struct XF<P_X3> {
+  bf16x8 h, l;
+};
+template <>
+struct XF<P_FP8> {
+  long q;   // 8 e4m3
+};
+template <int P>
+struct WF {  // A-role (weight) fragment
+  bf16x8 h;
+};
+template <>
+struct WF<P_X3> {
+  bf16x8 h, l;
+};
+template <>
+struct WF<P_FP8> {
+  long hi, lo;   // 16·⌊q/16⌋ and q mod 16, e4m3
+};
+
+__device__ __forceinline__ f32x4 mfma8(long a, long b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+}
+
+// W·X (weights as A): the transposed dense layer Yᵀ = W·Xᵀ
+template <int P>
+__device__ __forceinline__ f32x4 mma(const WF<P>& a, const XF<P>& b, f32x4 c) {
+  if constexpr (P == P_BF16) {
+    return mfma16x16x32(a.h, b.h, c);
+  } else if constexpr (P == P_X3) {
+    c = mfma16x16x32(a.l, b.h, c);   // small terms first
+    c = mfma16x16x32(a.h, b.l, c);
+    return mfma16x16x32(a.h, b.h, c);
+  } else {
+    c = mfma8(a.lo, b.q, c);
+    return mfma8(a.hi, b.q, c);
+  }
+}
+// X·Wᵀ (activations as A): V = X·Wvᵀ, whose C fragment is the A operand of Oᵀ = Vᵀ·Pᵀ
+template <int P>
+__device__ __forceinline__ f32x4 mma_xw(const XF<P>& a, const WF<P>& b, f32x4 c) {
+  if constexpr (P == P_BF16) {
+    return mfma16x16x32(a.h, b.h, c);
+  } else if constexpr (P == P_X3) {
+    c = mfma16x16x32(a.l, b.h, c);
+    c = mfma16x16x32(a.h, b.l, c);
+    return mfma16x16x32(a.h, b.h, c);
+  } else {
+    c = mfma8(a.q, b.lo, c);
+    return mfma8(a.q, b.hi, c);
+  }
+}
+
+// 16x16x16 operands of the attention products (Sᵀ = K·Qᵀ, Oᵀ = Vᵀ·Pᵀ): bf16, or hi/lo pairs in X3
+template <int P>
+struct AF {
+  bf16x4 h;
+};
+template <>
+struct AF<P_X3> {
+  bf16x4 h, l;
+};
+template <int P>
+__device__ __forceinline__ AF<P> split4(const f32x4& v) {
+  AF<P> r;
+  r.h = cvt4(v);
+  if constexpr (P == P_X3) r.l = cvt4(v - __builtin_convertvector(r.h, f32x4));
+  return r;
+}
+template <int P>
+__device__ __forceinline__ f32x4 mma16(const AF<P>& a, const AF<P>& b, f32x4 c) {
+  if constexpr (P == P_X3) {
+    c = mfma16x16x16(a.l, b.h, c);
+    c = mfma16x16x16(a.h, b.l, c);
+  }
+  return mfma16x16x16(a.h, b.h, c);
+}
+
+// fp32 → operand conversions
+template <int P>
+__device__ __forceinline__ XF<P> split8(const f32x4& a, const f32x4& b) {
+  XF<P> r;
+  r.h = cvt8(a, b);
+  if constexpr (P == P_X3) {
+    const bf16x4 ha = {r.h[0], r.h[1], r.h[2], r.h[3]}, hb = {r.h[4], r.h[5], r.h[6], r.h[7]};
+    r.l = cvt8(a - __builtin_convertvector(ha, f32x4), b - __builtin_convertvector(hb, f32x4));
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t fp8x4(const f32x4& v) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], w, true);
+  return (uint32_t)w;
+}
+
+// ------------------------------------------------------------------ LDS images
+// An activation image: `rows` × 128 features of plane(s) starting at byte `base` of the LDS window,
+// RS bytes per row; the X3 lo plane sits `lo` bytes after the hi plane.
+template <int P>
+struct ImgBase {   // the lo-plane offset exists only where there is a lo plane
+  char* base;
+  int lo;
+};
+template <>
+struct ImgBase<P_BF16> {
+  char* base;
+  static constexpr int lo = 0;
+};
+template <>
+struct ImgBase<P_FP8> {
+  char* base;
+  static constexpr int lo = 0;
+};
+template <int P>
+struct Img : ImgBase<P> {
+  using ImgBase<P>::base;
+  using ImgBase<P>::lo;
+  __device__ __forceinline__ Img(char* b, int l) {
+    base = b;
+    if constexpr (P == P_X3) this->lo = l;
+    (void)l;
+  }
+  __device__ __forceinline__ Img() = default;
+  __device__ __forceinline__ XF<P> ld(int row, int k0) const {
+    constexpr int RS = Geo<P>::RS;
+    XF<P> r;
+    if constexpr (P == P_FP8) {
+      r.q = *reinterpret_cast<const long*>(base + row * RS + k0);
+    } else {
+      r.h = *reinterpret_cast<const bf16x8*>(base + row * RS + 2 * k0);
+      if constexpr (P == P_X3) r.l = *reinterpret_cast<const bf16x8*>(base + lo + row * RS + 2 * k0);
+    }
+    return r;
+  }
+  __device__ __forceinline__ void st4(int row, int n0, const f32x4& v) const {
+    constexpr int RS = Geo<P>::RS;
+    if constexpr (P == P_FP8) {
+      *reinterpret_cast<uint32_t*>(base + row * RS + n0) = fp8x4(v);
+    } else {
+      const bf16x4 h = cvt4(v);
+      *reinterpret_cast<bf16x4*>(base + row * RS + 2 * n0) = h;
+      if constexpr (P == P_X3)
+        *reinterpret_cast<bf16x4*>(base + lo + row * RS + 2 * n0) = cvt4(v - __builtin_convertvector(h, f32x4));
+    }
+  }
+  __device__ __forceinline__ void st1(int row, int n, float v) const {
+    constexpr int RS = Geo<P>::RS;
+    if constexpr (P == P_FP8) {
+      *reinterpret_cast<uint8_t*>(base + row * RS + n) = (uint8_t)__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false);
+    } else {
+      const __bf16 h = (__bf16)v;
+      *reinterpret_cast<__bf16*>(base + row * RS + 2 * n) = h;
+      if constexpr (P == P_X3) *reinterpret_cast<__bf16*>(base + lo + row * RS + 2 * n) = (__bf16)(v - (float)h);
+    }
+  }
+};
+
+// B-operand loaders
+template <int P>
+struct LoadImg {
+  Img<P> im;
+  __device__ __forceinline__ XF<P> operator()(int m, int k0) const { return im.ld(m, k0); }
+};
+// Circular k=3 conv input: A[m][tap·128 + c] = X[(m-1+tap) mod L][c]
+template <int P>
+struct LoadCirc3 {
+  Img<P> im;
+  int L;
+  __device__ __forceinline__ XF<P> operator()(int m, int k0) const {
+    const int tap = k0 >> 7, c = k0 & 127;
+    int r = m - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded rows only
+    return im.ld(r, c);
+  }
+};
+// Token-embedding input for output row m = position m + off (EncoderStack window):
+// A[m][tap·C + c] = x[(m + off - 1 + tap) mod L][c], zero past 3·C (C a power of two).  The embedding
+// is never quantised: P here is plain_of<>.
+template <int P>
+struct LoadEmbed {
+  const float* X;
+  int L, CSH, CS, off;
+  __device__ __forceinline__ XF<P> operator()(int m, int k0) const {
+    const int tap = k0 >> CSH, c = k0 & ((1 << CSH) - 1);
+    if (tap >= 3) return XF<P>{};
+    int r = m + off - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded rows (m >= L) only: any valid row
+    const f32x4* p = reinterpret_cast<const f32x4*>(X + r * CS + c);
+    return split8<P>(p[0], p[1]);
+  }
+};
+
+// ------------------------------------------------------------------ weights and parameters
+struct Mem {
+  __amdgpu_buffer_rsrc_t w;   // packed fragments [n_tile][k_step][lane][16 B]
+  __amdgpu_buffer_rsrc_t p;   // fp32 parameter blob
+  uint32_t wlo;               // X3: byte offset of the lo-fragment blob
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ uint4 wload16(const Mem& m, uint32_t off, int lane) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(m.w, lane * 16, (int)off, 0));
+}
+// this lane's fragment of the 1 KiB wave tile at uniform byte offset `off`
+template <int P>
+__device__ __forceinline__ WF<P> wfrag(const Mem& m, uint32_t off, int lane) {
+  WF<P> r;
+  const uint4 v = wload16(m, off, lane);
+  if constexpr (P == P_FP8) {
+    r.hi = (long)(((unsigned long long)v.y << 32) | v.x);
+    r.lo = (long)(((unsigned long long)v.w << 32) | v.z);
+  } else {
+    r.h = __builtin_bit_cast(bf16x8, v);
+    if constexpr (P == P_X3) r.l = __builtin_bit_cast(bf16x8, wload16(m, off + m.wlo, lane));
+  }
+  return r;
+}
+__device__ __forceinline__ f32x4 pload4(const Mem& m, uint32_t so, int vo) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(m.p, vo * 4, (int)(so * 4u), 0));
+}
+__device__ __forceinline__ float pload1(const Mem& m, uint32_t so, int vo) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(m.p, vo * 4, (int)(so * 4u), 0));
+}
+__device__ __forceinline__ f32x4 load4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// Lane index the compiler cannot hoist (keeps lane-derived addresses from living across phases).
+__device__ __forceinline__ int lane_op() {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
+template <int P, int KS>
+__device__ __forceinline__ void load_frags(const Mem& m, uint32_t base, int nt, WF<P> (&a)[KS]) {
+  const int lane = lane_op();
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) a[ks] = wfrag<P>(m, base * 16u + (uint32_t)(nt * KS + ks) * 1024u, lane);
+}
+__device__ __forceinline__ void epi_vecs(const Mem& m, const GemmDesc& d, int n0, f32x4& sc, f32x4& bi) {
+  sc = f32x4{1.f, 1.f, 1.f, 1.f};
+  bi = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (d.scale != NONE) sc = pload4(m, d.scale, n0);
+  if (d.bias != NONE) bi = pload4(m, d.bias, n0);
+}
+
+template <int N>
+struct Res {
+  f32x4 v[N];
+};
+
+// A dense layer's per-wave operands, requested ahead of the barrier that precedes the layer.
+template <int P, int KS>
+struct WPre {
+  WF<P> a[KS];
+  f32x4 sc, bi;
+};
+template <int P, int KS>
+__device__ __forceinline__ WPre<P, KS> prefetch_res(const Mem& m, const GemmDesc d) {
+  WPre<P, KS> p;
+  const int lane = lane_op(), w = wave_id();
+  load_frags<P, KS>(m, d.w, w, p.a);
+  epi_vecs(m, d, 16 * w + (lane >> 4) * 4, p.sc, p.bi);
+  return p;
+}
+
+// Dense layer whose output n-tile w lands in the wave's residual fragments (runtime m-tile count).
+template <int P, int KS, int N, class BL, class Epi>
+__device__ __forceinline__ void gemm_res(const WPre<P, KS>& p, int nmt, BL&& bl, Epi&& epi) {
+  const int lane = lane_op(), w = wave_id();
+  const int n0 = 16 * w + (lane >> 4) * 4;
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) c = mma<P>(p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+      epi(mt, n0, c * p.sc + p.bi);
+    }
+  }
+}
+template <int P, int KS, int N, class BL, class Epi>
+__device__ __forceinline__ void gemm_res(const Mem& m, const GemmDesc d, int nmt, BL&& bl, Epi&& epi) {
+  gemm_res<P, KS, N>(prefetch_res<P, KS>(m, d), nmt, bl, epi);
+}
+
+// Compile-time m-tile count: B fragments of tile mt+1 requested before the MFMAs of tile mt.
+template <int P, int KS, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_res_n(const WPre<P, KS>& p, BL&& bl, Epi&& epi) {
+  const int lane = lane_op(), w = wave_id();
+  const int n0 = 16 * w + (lane >> 4) * 4;
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  XF<P> b[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) b[ks] = bl(mrow, ks * 32 + kq);
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    XF<P> bn[KS];
+    if (mt + 1 < NMT) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bn[ks] = bl((mt + 1) * 16 + mrow, ks * 32 + kq);
+    }
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) c = mma<P>(p.a[ks], b[ks], c);
+    epi(mt, n0, c * p.sc + p.bi);
+    if (mt + 1 < NMT) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) b[ks] = bn[ks];
+    }
+  }
+}
+template <int P, int KS, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_res_n(const Mem& m, const GemmDesc d, BL&& bl, Epi&& epi) {
+  gemm_res_n<P, KS, NMT>(prefetch_res<P, KS>(m, d), bl, epi);
+}
+
+// Dense layer over an arbitrary n-tile count (the projection), output through epi only.
+template <int P, int KS, class BL, class Epi>
+__device__ __forceinline__ void gemm_tiles(const Mem& m, const GemmDesc d, int n_tiles, int nmt, BL&& bl, Epi&& epi) {
+  const int lane = lane_op(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  int nt0 = w, nt_step = NW, mt0 = 0, mt_step = 1;
+  if (n_tiles < NW) {
+    const int per = NW / n_tiles;
+    if (w >= per * n_tiles) return;
+    nt0 = w % n_tiles;
+    nt_step = n_tiles;
+    mt0 = w / n_tiles;
+    mt_step = per;
+  }
+  for (int nt = nt0; nt < n_tiles; nt += nt_step) {
+    WF<P> a[KS];
+    load_frags<P, KS>(m, d.w, nt, a);
+    const int n0 = nt * 16 + (lane >> 4) * 4;
+    f32x4 sc, bi;
+    epi_vecs(m, d, n0, sc, bi);
+    for (int mt = mt0; mt < nmt; mt += mt_step) {
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) c = mma<P>(a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+      epi(mt, n0, c * sc + bi);
+    }
+  }
+}
+
+// n_tiles ≤ NW (FFN hidden): wave w takes n-tile w mod n_tiles and every (NW / n_tiles)-th m-tile.
+template <int P, int KS>
+__device__ __forceinline__ WPre<P, KS> prefetch_tiles(const Mem& m, const GemmDesc d, int n_tiles) {
+  WPre<P, KS> p;
+  const int lane = lane_op(), w = wave_id();
+  const int nt = w % n_tiles;
+  load_frags<P, KS>(m, d.w, nt, p.a);
+  epi_vecs(m, d, nt * 16 + (lane >> 4) * 4, p.sc, p.bi);
+  return p;
+}
+template <int P, int KS, class BL, class Epi>
+__device__ __forceinline__ void gemm_tiles1(const WPre<P, KS>& p, int n_tiles, int nmt, BL&& bl, Epi&& epi) {
+  const int lane = lane_op(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int per = NW / n_tiles;
+  if (w >= per * n_tiles) return;
+  const int nt = w % n_tiles, mt_step = per;
+  const int n0 = nt * 16 + (lane >> 4) * 4;
+  for (int mt = w / n_tiles; mt < nmt; mt += mt_step) {
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) c = mma<P>(p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+    epi(mt, n0, c * p.sc + p.bi);
+  }
+}
+
+// Deep-K dense layer (the distil conv, K = 384) in k-outer order with a compile-time m-tile count:
+// one accumulator per m-tile, the B fragments of step ks+1 requested before step ks's MFMAs, and the
+// weight fragments loaded in groups of KH k-steps.
+template <int P, int KS, int KH>
+__device__ __forceinline__ WPre<P, KH> prefetch_kouter(const Mem& m, const GemmDesc d) {
+  WPre<P, KH> p;
+  const int lane = lane_op(), w = wave_id();
+#pragma unroll
+  for (int ks = 0; ks < KH; ++ks) p.a[ks] = wfrag<P>(m, d.w * 16u + (uint32_t)(w * KS + ks) * 1024u, lane);
+  epi_vecs(m, d, 16 * w + (lane >> 4) * 4, p.sc, p.bi);
+  return p;
+}
+template <int P, int KS, int KH, int NMT, class BL, class Epi>
+__device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem& m, const GemmDesc d, BL&& bl,
+                                                Epi&& epi) {
+  static_assert(KS % KH == 0, "k-steps split into equal groups");
+  const int lane = lane_op(), w = wave_id();
+  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int n0 = 16 * w + (lane >> 4) * 4;
+  const f32x4 sc = p.sc, bi = p.bi;
+  f32x4 c[NMT];
+  XF<P> b[NMT];
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    c[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    b[mt] = bl(mt * 16 + mrow, kq);
+  }
+  const uint32_t t0 = d.w * 16u + (uint32_t)(w * KS) * 1024u;
+#pragma unroll
+  for (int hf = 0; hf < KS / KH; ++hf) {
+    WF<P> a[KH];
+#pragma unroll
+    for (int ks = 0; ks < KH; ++ks) a[ks] = hf == 0 ? p.a[ks] : wfrag<P>(m, t0 + (uint32_t)(hf * KH + ks) * 1024u, lane);
+#pragma unroll
+    for (int ks = 0; ks < KH; ++ks) {
+      const int kk = hf * KH + ks;
+      XF<P> bn[NMT];
+      if (kk + 1 < KS) {
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) bn[mt] = bl(mt * 16 + mrow, (kk + 1) * 32 + kq);
+      }
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) c[mt] = mma<P>(a[ks], b[mt], c[mt]);
+      if (kk + 1 < KS) {
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) b[mt] = bn[mt];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch distance at one k-step
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) epi(mt, n0, c[mt] * sc + bi);
+}
+
+// LayerNorm of the register residual over all 128 features (8 waves × 16): each wave reduces its
+// 16 features per row to (mean_w, M2_w), the 8 pairs meet in LDS, Chan's combination gives the
+// exact row statistics.  Normalised rows go to X and rows < `rows` to the image `out` (and `out2`).
+// torch.nn.LayerNorm (biased var, eps in the sqrt) or, if unbiased_std, the reference Transformer's
+// LayerNormalization.  One workgroup barrier inside; the caller adds one before the image is read.
+template <int N, class Out, class Out2>
+__device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
+                                       bool unbiased_std, float* part, const Out& out, const Out2* out2) {
+  const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
+  const int nb = 16 * w + 4 * g;
+  const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barrier
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      float s = (X.v[mt][0] + X.v[mt][1]) + (X.v[mt][2] + X.v[mt][3]);
+      s = xor_sum(s, 16);
+      s = xor_sum(s, 32);
+      const float mw = s * (1.0f / 16.0f);
+      float q = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = X.v[mt][r] - mw;
+        q = fmaf(d, d, q);
+      }
+      q = xor_sum(q, 16);
+      q = xor_sum(q, 32);
+      if (g == 0) *reinterpret_cast<f32x2*>(part + (mt * 16 + c) * LN_STRIDE + 2 * w) = f32x2{mw, q};
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      const int m = mt * 16 + c;
+      const float* pr = part + m * LN_STRIDE;
+      const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
+      const float mean = 0.125f * (((p0[0] + p0[2]) + (p1[0] + p1[2])) + ((p2[0] + p2[2]) + (p3[0] + p3[2])));
+      const float d0 = p0[0] - mean, d1 = p0[2] - mean, d2 = p1[0] - mean, d3 = p1[2] - mean;
+      const float d4 = p2[0] - mean, d5 = p2[2] - mean, d6 = p3[0] - mean, d7 = p3[2] - mean;
+      const float M2 = (((p0[1] + p0[3]) + (p1[1] + p1[3])) + ((p2[1] + p2[3]) + (p3[1] + p3[3]))) +
+                       16.0f * ((d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3) + (d4 * d4 + d5 * d5 + d6 * d6 + d7 * d7));
+      const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
+                                     : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
+      X.v[mt] = (X.v[mt] - mean) * inv * g0 + b0;
+      if (m < rows) {
+        out.st4(m, nb, X.v[mt]);
+        if (out2) out2->st4(m, nb, X.v[mt]);
+      }
+    }
+  }
+}
+
+// image of the register residual (rows < rows)
+template <int N, class Out>
+__device__ __forceinline__ void store_res(const Res<N>& X, int nmt, int rows, const Out& out) {
+  const int lane = lane_op(), w = wave_id();
+  const int nb = 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      const int m = mt * 16 + (lane & 15);
+      if (m < rows) out.st4(m, nb, X.v[mt]);
+    }
+  }
+}
+
+// fp32 dump of the register residual rows < rows into dst[rows][128] (debug only).
+template <int N>
+__device__ __forceinline__ void dump_res(const Res<N>& X, int nmt, int rows, float* dst) {
+  const int lane = lane_op(), w = wave_id();
+  const int nb = 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      const int m = mt * 16 + (lane & 15);
+      if (m < rows) *reinterpret_cast<f32x4*>(dst + m * DMODEL + nb) = X.v[mt];
+    }
+  }
+}
+
+// Calls f(std::integral_constant<int, n>) for the runtime m-tile count n in [1, MT].
+template <class F>
+__device__ __forceinline__ void with_nmt(int n, F&& f) {
+  switch (n) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    default: f(std::integral_constant<int, 6>{}); break;
+  }
+}
+
+// MaxPool1d(kernel 3, stride 2, padding 1) over positions of a register-resident tile set:
+// out row t' = max(x[2t'-1], x[2t'], x[2t'+1]) over rows in [0, L).  Rows live on the 16-lane
+// axis, so the 2:1 gather is a within-row ds_bpermute from tiles 2j-1, 2j, 2j+1.
+template <int NIN>
+__device__ __forceinline__ void maxpool_res(const Res<NIN>& in, int L, Res<MT>& out) {
+  const int lane = lane_op();
+  const int c = lane & 15, base = lane & 48;
+  const int s0 = base | ((2 * c) & 15), s1 = base | ((2 * c + 1) & 15), sm = base | ((2 * c - 1) & 15);
+  constexpr int NOUT = (NIN + 1) / 2;
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a0 = __shfl(in.v[2 * j][r], s0, 64);
+      const float a1 = __shfl(in.v[2 * j][r], s1, 64);
+      const float a2 = __shfl(in.v[2 * j][r], sm, 64);
+      float b0 = 0.f, b1 = 0.f, b2 = 0.f;   // tile 2j+1 absent: only padded output rows read it
+      if (2 * j + 1 < NIN) {
+        b0 = __shfl(in.v[2 * j + 1][r], s0, 64);
+        b1 = __shfl(in.v[2 * j + 1][r], s1, 64);
+        b2 = __shfl(in.v[2 * j + 1][r], sm, 64);
+      }
+      const float c2 = j > 0 ? __shfl(in.v[(2 * j - 1 < 0) ? 0 : 2 * j - 1][r], sm, 64) : NEG_INF;
+      const int row0 = 32 * j + 2 * c;
+      float v = c < 8 ? a0 : b0;                          // row 2t'   (always < L for t' < L_out)
+      const float v1 = c < 8 ? a1 : b1;                   // row 2t'+1
+      const float vm = c == 0 ? c2 : (c <= 8 ? a2 : b2);  // row 2t'-1
+      if (row0 + 1 < L) v = fmaxf(v, v1);
+      if (row0 - 1 >= 0) v = fmaxf(v, vm);
+      out.v[j][r] = v;
+    }
+  }
+#pragma unroll
+  for (int j = NOUT; j < MT; ++j) out.v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// ------------------------------------------------------------------------------ attention
+// One head per wave, everything in registers: Kᵀ = Wk_h·Xᵀ (A of Sᵀ = K·Qᵀ), Qᵀ = Wq_h·Xᵀ (B of Sᵀ),
+// V = X·Wv_hᵀ (A of Oᵀ = Vᵀ·Pᵀ), and the exponentiated Sᵀ tile is the B fragment of Oᵀ.
+// Reference: attn.py:73-175 (ProbAttention), :37-70 (FullAttention), :195-209 (AttentionLayer, mix).
+// PD: precision of the Q/K/V projections (the model's dense policy); PA: of the attention products.
+template <int PD>
+struct HeadIO {
+  Img<PD> xq, xkv;            // images feeding the queries / keys+values
+  Img<PD> ctx;                // attention context out (the O-projection's input image)
+  uint32_t wq, wk, wv;        // weight-blob offsets (16-byte units) of n-tile 0 of each projection
+  GemmDesc dq, dk, dv;        // epilogue vectors (bias/scale offsets at the part's start)
+  int LQ, LK, prob, causal, mix, u;
+  const uint8_t* cnt;
+  int cnt_stride;
+  float* scr;                 // per-wave scratch: keys [96] u64, sel [96] int16, flag [96] bytes
+  float* attn_out;            // global [H][LQ][LK] of this sequence or nullptr
+  float* m_dbg;               // global [H][LQ] or nullptr
+  unsigned long long* st;     // diagnostics: sub-phase s_memtime stamps of head 0, or nullptr
+};
+
+template <int PD, int MQ = MT, int MK = MT>
+__device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h) {
+  constexpr int PA = plain_of<PD>();
+  const int lane = lane_op();
+  const int col = lane & 15, g = lane >> 4;
+  const int LQ = io.LQ, LK = io.LK;
+  const int nkt = (LK + 15) >> 4, nqt = (LQ + 15) >> 4;
+  const bool sparse = io.prob && io.u < LQ;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(io.scr);
+  int16_t* sel = reinterpret_cast<int16_t*>(io.scr + 192);
+  uint8_t* flag = reinterpret_cast<uint8_t*>(io.scr + 240);
+  auto SUB = [&](int k) {
+    if (io.st && h == 0 && lane == 0) io.st[k] = __builtin_amdgcn_s_memtime();
+  };
+  SUB(0);
+  const int fq = 16 * h + 4 * g;
+  const int kq = g * 8;
+  AF<PA> Kf[MK], Vf[MK];
+  {
+    // pass 1: K and V tiles from the key/value rows
+    WF<PD> wk[4], wv[4];
+    load_frags<PD, 4>(m, io.wk, h, wk);
+    load_frags<PD, 4>(m, io.wv, h, wv);
+    f32x4 sk, bk;
+    epi_vecs(m, io.dk, fq, sk, bk);
+    const float sv = io.dv.scale != NONE ? pload1(m, io.dv.scale, 16 * h + col) : 1.f;
+    const float bv = io.dv.bias != NONE ? pload1(m, io.dv.bias, 16 * h + col) : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MK; ++mt) {
+      Kf[mt] = AF<PA>{};
+      Vf[mt] = AF<PA>{};
+      if (mt < nkt) {
+        f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = k;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const XF<PD> bx = io.xkv.ld(mt * 16 + col, ks * 32 + kq);
+          k = mma<PD>(wk[ks], bx, k);
+          v = mma_xw<PD>(bx, wv[ks], v);
+        }
+        Kf[mt] = split4<PA>(k * sk + bk);
+        Vf[mt] = split4<PA>(v * sv + bv);
+      }
+    }
+  }
+  SUB(1);
+  // Q tiles are projected where they are consumed (per query tile in M, per selected tile in the
+  // softmax): wq and its epilogue vectors are the only Q state that lives
+  WF<PD> wq[4];
+  load_frags<PD, 4>(m, io.wq, h, wq);
+  f32x4 sq, bq;
+  epi_vecs(m, io.dq, fq, sq, bq);
+  auto project_q = [&](int row) __attribute__((always_inline)) {
+    f32x4 q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) q = mma<PD>(wq[ks], io.xq.ld(row, ks * 32 + kq), q);
+    return split4<PA>(q * sq + bq);
+  };
+
+  SUB(2);
+  if (sparse) {
+    // ---- sparsity measurement M (attn.py:95-105) from key multiplicities (LDS-staged table)
+    const float invLK = 1.0f / (float)LK;
+#pragma unroll
+    for (int qt = 0; qt < MQ; ++qt) {
+      if (qt >= nqt) break;
+      const int q = qt * 16 + col;
+      const AF<PA> qf = project_q(q);
+      // this lane's six count words (keys 16kt + 4g + r, kt = 0..5) are contiguous (cnt_pos_v2)
+      const uint2* crow = reinterpret_cast<const uint2*>(io.cnt + (size_t)q * io.cnt_stride + g * 24);
+      const uint2 c01 = crow[0], c23 = crow[1], c45 = crow[2];
+      const uint32_t cws[MT] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
+      float sum = 0.f, mx = NEG_INF;
+#pragma unroll
+      for (int kt = 0; kt < MK; ++kt) {
+        if (kt < nkt) {
+          const f32x4 s = mma16<PA>(Kf[kt], qf, f32x4{0.f, 0.f, 0.f, 0.f});
+          const uint32_t cw = cws[kt];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float cf = (float)((cw >> (8 * r)) & 0xffu);
+            sum = fmaf(cf, s[r], sum);
+            mx = fmaxf(mx, cf != 0.f ? s[r] : NEG_INF);
+          }
+        }
+      }
+      sum = xor_sum(sum, 16);
+      sum = xor_sum(sum, 32);
+      mx = xor_max(mx, 16);
+      mx = xor_max(mx, 32);
+      const float M = mx - sum * invLK;
+      // selection key: order-preserving image of M above, ~q below — equal M go to the lower index
+      const uint32_t mu = __float_as_uint(M);
+      const uint32_t hi = (mu & 0x80000000u) ? ~mu : (mu | 0x80000000u);
+      const uint64_t key = q < LQ ? ((uint64_t)hi << 32) | (uint32_t)(0xffff - q) : 0ull;
+      if (g == 0) {
+        keys[q] = key;
+        if (io.m_dbg && q < LQ) io.m_dbg[h * LQ + q] = M;
+      }
+    }
+    wave_lds_sync();
+    SUB(3);
+    // ---- exact top-u by rank: rank(q) = #{j : key_j > key_q}; q is selected iff rank < u and
+    //      lands in sel[rank].  Lane group g counts over keys [g·J, g·J + J), J = 4·nqt.
+    uint64_t myk[MQ];
+    int rank[MQ];
+#pragma unroll
+    for (int qt = 0; qt < MQ; ++qt) {
+      myk[qt] = qt < nqt ? keys[qt * 16 + col] : ~0ull;
+      rank[qt] = 0;
+    }
+    const int J = 4 * nqt;
+    const uint64_t* kg = keys + g * J;
+#pragma unroll 2
+    for (int j = 0; j < J; j += 2) {
+      const u64x2 kk = *reinterpret_cast<const u64x2*>(kg + j);
+#pragma unroll
+      for (int qt = 0; qt < MQ; ++qt) rank[qt] += (int)(kk[0] > myk[qt]) + (int)(kk[1] > myk[qt]);
+    }
+    const int uu = io.u;
+#pragma unroll
+    for (int qt = 0; qt < MQ; ++qt) {
+      if (qt < nqt) {
+        int r = rank[qt];
+        r = (int)xor_sum((float)r, 16);     // counts < 2^24: exact in fp32
+        r = (int)xor_sum((float)r, 32);
+        const int q = qt * 16 + col;
+        if (g == 0 && q < LQ) {
+          const bool s = r < uu;
+          flag[q] = s;
+          if (s) sel[r] = (int16_t)q;
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+  auto ctx_st4 = [&](int q, int e0, const f32x4& v) __attribute__((always_inline)) {
+    if (!io.mix) {
+      io.ctx.st4(q, h * 16 + e0, v);
+    } else {
+      const int f = h * LQ * 16 + q * 16 + e0;   // (L,H,E) values re-viewed as (H,L,E) memory
+      io.ctx.st4(f >> 7, f & 127, v);
+    }
+  };
+  if (sparse && !io.causal) {
+    // ---- unselected rows keep the initial context, mean(V) (attn.py:116-119): written to every
+    //      row here, then the selected rows are overwritten below (same wave, LDS in order)
+    float part = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < MK; ++kt)
+      if (kt < nkt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = (float)Vf[kt].h[j];
+          if constexpr (PA == P_X3) v += (float)Vf[kt].l[j];
+          part += (kt * 16 + g * 4 + j < LK) ? v : 0.f;
+        }
+    part = xor_sum(part, 16);
+    part = xor_sum(part, 32);
+    const float mean = part / (float)LK;
+    if (!io.mix) {
+      for (int q = g; q < LQ; q += 4) io.ctx.st1(q, h * 16 + col, mean);
+    } else {
+      for (int q = g; q < LQ; q += 4) {
+        const int f = h * LQ * 16 + q * 16 + col;
+        io.ctx.st1(f >> 7, f & 127, mean);
+      }
+    }
+  }
+  SUB(4);
+
+  // ---- softmax(scale·q·Kᵀ [mask])·V for the selected queries (attn.py:109-138 / 57-65)
+  const float scale = 0.25f;
+  const int nsel = sparse ? io.u : LQ;
+  const int nst = (nsel + 15) >> 4;
+#pragma unroll 1
+  for (int st = 0; st < nst; ++st) {
+    const int i = st * 16 + col;
+    const int ic = i < nsel ? i : nsel - 1;
+    const int qi = sparse ? (int)sel[ic] : ic;
+    const AF<PA> qs = project_q(qi);
+    float mx = NEG_INF;
+#pragma unroll
+    for (int kt = 0; kt < MK; ++kt) {
+      if (kt < nkt) {
+        const f32x4 a = mma16<PA>(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + g * 4 + r;
+          const bool masked = key >= LK || (io.causal && key > qi);
+          mx = masked ? mx : fmaxf(mx, a[r] * scale);
+        }
+      }
+    }
+    mx = xor_max(mx, 16);
+    mx = xor_max(mx, 32);
+    float sum = 0.f;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < MK; ++kt) {
+      if (kt < nkt) {
+        f32x4 p = mma16<PA>(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + g * 4 + r;
+          const bool masked = key >= LK || (io.causal && key > qi);
+          p[r] = masked ? 0.f : __expf(p[r] * scale - mx);
+          sum += p[r];
+        }
+        o = mma16<PA>(Vf[kt], split4<PA>(p), o);
+      }
+    }
+    sum = xor_sum(sum, 16);
+    sum = xor_sum(sum, 32);
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    if (i < nsel) {
+      ctx_st4(qi, g * 4, o * inv);
+      if (io.attn_out) {
+        float* arow = io.attn_out + ((size_t)h * LQ + qi) * LK;
+#pragma unroll
+        for (int kt = 0; kt < MK; ++kt)
+          if (kt < nkt) {
+            const f32x4 p = mma16<PA>(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = kt * 16 + g * 4 + r;
+              const bool masked = key >= LK || (io.causal && key > qi);
+              if (key < LK) arow[key] = masked ? 0.f : __expf(p[r] * scale - mx) * inv;
+            }
+          }
+      }
+    }
+  }
+
+  SUB(5);
+  if (sparse) {
+    if (io.causal) {
+      // masked: unselected rows keep cumsum(V) (attn.py:120-125) = Vᵀ·Tᵀ with T[q][key] = [key <= q]
+#pragma unroll
+      for (int qt = 0; qt < MQ; ++qt) {
+        if (qt < nqt) {
+          const int q = qt * 16 + col;
+          f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kt = 0; kt < MK; ++kt) {
+            if (kt < nkt) {
+              f32x4 ind;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int key = kt * 16 + g * 4 + r;
+                ind[r] = (key <= q && key < LK) ? 1.f : 0.f;
+              }
+              o = mma16<PA>(Vf[kt], split4<PA>(ind), o);
+            }
+          }
+          if (q < LQ && !flag[q]) ctx_st4(q, g * 4, o);
+        }
+      }
+    }
+    if (io.attn_out) {
+      const float invL = 1.0f / (float)LK;
+      for (int q = 0; q < LQ; ++q)
+        if (!flag[q]) {
+          float* arow = io.attn_out + ((size_t)h * LQ + q) * LK;
+          for (int k = lane; k < LK; k += WAVE) arow[k] = invL;
+        }
+    }
+  }
+  SUB(6);
+}
+
+}  // namespace v4
+}  // namespace cet

@@ -114,6 +114,25 @@ class Engine:
                               ctypes.c_void_p(attns.data_ptr()) if attns is not None else None,
                               ctypes.c_void_p(stream)), "cet_forward")
 
+    def forward_nmse(self, x_enc, x_dec, out, label, nmse_acc=None, nmse_sums=None, stream: Optional[int] = None):
+        """Forward + NMSE_Split(out, label) in one launch (cet_forward_nmse): ``nmse_acc`` float32 [T] += the
+        batch's ratio, ``nmse_sums`` float64 [2, T] = its raw sums (either may be None, not both)."""
+        import torch
+
+        B, T = int(x_enc.shape[0]), int(out.shape[1])
+        if tuple(label.shape) != tuple(out.shape) or label.dtype != torch.float32 or not label.is_contiguous():
+            raise ValueError("label must be a contiguous float32 tensor shaped like out")
+        if nmse_acc is not None and (nmse_acc.dtype != torch.float32 or nmse_acc.numel() != T):
+            raise ValueError(f"nmse_acc must be float32 [{T}]")
+        if nmse_sums is not None and (nmse_sums.dtype != torch.float64 or nmse_sums.numel() != 2 * T
+                                      or not nmse_sums.is_contiguous()):
+            raise ValueError(f"nmse_sums must be a contiguous float64 [2, {T}]")
+        if stream is None:
+            stream = _stream_ptr(x_enc.device)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        check(lib.cet_forward_nmse(self._h, ptr(x_enc), ptr(x_dec), B, ptr(out), ptr(label), ptr(nmse_acc),
+                                   ptr(nmse_sums), ctypes.c_void_p(stream)), "cet_forward_nmse")
+
     def attns_floats(self) -> int:
         return check(lib.cet_attns_floats(self._h), "cet_attns_floats")
 
@@ -133,8 +152,19 @@ class Engine:
         check(lib.cet_set_sampler(self._h, int(bool(on_host))), "cet_set_sampler")
 
     def set_variant(self, variant: int) -> None:
-        """Fused-kernel generation: 3 (register-resident, default) or 1 (LDS-resident)."""
+        """Fused-kernel generation: 4 (default), 3 (bf16-only predecessor) or 1 (LDS-resident)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
+
+    PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2}
+
+    def set_precision(self, prec) -> None:
+        """Dense-layer operand precision of the v4 kernel: "auto", "bf16", "split-bf16" or "fp8" (include/cet.h)."""
+        code = self.PRECISIONS[prec] if isinstance(prec, str) else int(prec)
+        check(lib.cet_set_precision(self._h, code), "cet_set_precision")
+
+    def precision(self) -> str:
+        code = check(lib.cet_get_precision(self._h), "cet_get_precision")
+        return {v: k for k, v in self.PRECISIONS.items()}[code]
 
     # ------------------------------------------------------------------ kernel timing
     def timing(self, enable: bool) -> None:

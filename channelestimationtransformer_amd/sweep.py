@@ -72,7 +72,7 @@ def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=Non
     """Yields one result dict per SNR (identical on every rank)."""
     import torch
 
-    from .engine import nmse_split, nmse_split_sums
+    from .engine import nmse_split
     from .pipeline import DeviceSeqData, synth_channels
     from .sharding import check_gathered_nmse, collate_step_sums, gather_predictions
 
@@ -104,8 +104,7 @@ def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=Non
             off = (i * world + rank) * batch
             xe, xd, lb = data.batch(idx=perm[off:off + batch], seed=seed, counter=(k << 32) + i * world + rank,
                                     snr=snr, out=bufs, stream=stream)
-            eng.forward(xe, xd, out, None, stream)
-            nmse_split_sums(out, lb, sums[i], stream=stream)
+            eng.forward_nmse(xe, xd, out, lb, None, sums[i], stream)   # forward + NMSE_Split, one launch
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
         if dist is not None:

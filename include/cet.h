@@ -97,6 +97,15 @@ int64_t cet_peek_draw(cet_engine* e, int32_t* out, int64_t n_max);
  * sequence block of cet_attns_floats() floats; layer views via cet_attns_layout(). */
 int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
                 void* stream);
+/* The validation step of run_validation (FullPrecision/QuantizationAwareTraining.py:115-122):
+ * out = model(x_enc, x_dec) and NMSELossSplit(out, label) (metrics.py:26-39) in one launch — the
+ * v4 kernel computes each sequence's per-step (Σ(x − x̂)², Σx̂²) in its projection epilogue and the
+ * last workgroup to finish reduces them over the batch in a fixed order (fp64).  label [B][out_len]
+ * [c_out] device fp32; nmse_acc [out_len] fp32 (+= the batch's ratio) and/or nmse_sums [2][out_len]
+ * fp64 (the raw sums, overwritten) may be NULL, not both.  Other kernels / c_out > 16: the forward
+ * then the standalone reduction on the same stream. */
+int cet_forward_nmse(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, const float* label,
+                     float* nmse_acc, double* nmse_sums, void* stream);
 int64_t cet_attns_floats(cet_engine* e);
 int cet_attns_layout(cet_engine* e, int64_t* offsets, int* lengths, int max);
 
@@ -107,10 +116,24 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen);
 /* Diagnostics (DIAG kernel instance): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
 
-/* Select the fused-kernel generation of an Informer engine: 3 (default, 8-wave register-resident,
- * two sequences per CU) or 1 (LDS-resident, one sequence per CU).
- * CET_KERNEL=v1 in the environment selects 1 at creation. */
+/* Select the fused-kernel generation of an Informer engine: 4 (default: 8-wave register-resident,
+ * two sequences per CU, precision policies), 3 (its bf16-only predecessor) or 1 (LDS-resident, one
+ * sequence per CU).  CET_KERNEL=v1 / v3 in the environment selects 1 / 3 at creation. */
 int cet_set_variant(cet_engine* e, int variant);
+
+/* Operand precision of the v4 kernel's dense layers (Informer engines):
+ *   -1 auto (default): 0, or 1 where bf16 cannot carry the model — an LSQ integer grid with |q| > 256,
+ *      or a genuinely sparse masked decoder (u < label_len + out_len), whose output is discontinuous
+ *      in the top-u selection;
+ *    0 bf16 operands, fp32 accumulation / LayerNorm / softmax (the C2 contract);
+ *    1 split bf16 (hi + lo per operand, three MFMAs per product): fp32-level parity;
+ *    2 fp8 (OCP e4m3) activations on the fp8 MFMA for the LSQ-quantised layers, the integer weight
+ *      grid carried exactly as two e4m3 parts (LSQ engines of at most 8 bits).
+ * cet_get_precision() returns the precision the packed plan uses (packs the weights if needed).
+ * Replaces nothing in the reference, which computes in fp32 (FullPrecision/InformerModel) or with
+ * fp32 fake-quantised weights (models/InformerLSQ/LSQ.py:65-74). */
+int cet_set_precision(cet_engine* e, int prec);
+int cet_get_precision(cet_engine* e);
 
 /* Where the native sampler (after cet_seed) runs for variant 3: 0 = on the device (the
  * resident mt19937, default), 1 = on the host (the same torch-compatible stream drawn by the host

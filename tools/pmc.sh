@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (one rocprofv3 run per counter group) over tools/run_forward.py; outputs in gpurun_out/$1
 set -euo pipefail
-TAG=${1:-pmc}; V=${2:-2}
+TAG=${1:-pmc}; V=${2:-4}
 R=$(pwd); O=$R/gpurun_out/$TAG; mkdir -p "$O"; export TMPDIR=/tmp; cd /tmp
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \

@@ -14,7 +14,7 @@ from channelestimationtransformer_amd.dataset import make_batch  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
-V = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+V = int(sys.argv[3]) if len(sys.argv) > 3 else 4
 dev = torch.device("cuda:0")
 m = bench.build_model(dev)
 eng = m.engine(dev)

@@ -1,6 +1,6 @@
-"""Per-phase cycle breakdown of the v2 fused kernel from in-kernel s_memtime stamps.
+"""Per-phase cycle breakdown of the fused kernel (DIAG instance) from in-kernel s_memtime stamps.
 
-Usage (GPU box): python tools/stamps.py [B] > gpurun_out/stamps.txt
+Usage (GPU box): python tools/stamps.py [B] [variant] > gpurun_out/stamps.txt
 """
 import os
 import sys
@@ -26,6 +26,8 @@ def main():
     dev = torch.device("cuda:0")
     m = bench.build_model(dev)
     eng = m.engine(dev)
+    if len(sys.argv) > 2:
+        eng.set_variant(int(sys.argv[2]))
     eng.seed(1)
     xe, xd, _ = make_batch(B, seed=5)
     xe = torch.from_numpy(xe).to(dev)
