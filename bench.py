@@ -135,6 +135,8 @@ def parse_args(argv=None):
                     help="fused-kernel generation (1: LDS-resident, 3/4: 8-wave register-resident)")
     ap.add_argument("--sampler", choices=("device", "host"), default="device",
                     help="where the native ProbSparse draws run (identical streams; DESIGN §3.3)")
+    ap.add_argument("--nmse", choices=("fused", "separate"), default="fused",
+                    help="NMSE_Split in the forward's epilogue (cet_forward_nmse) or as its own launch")
     ap.add_argument("--collation-selftest", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank spawn and NMSE collation (no GPU, no engine)")
     return ap.parse_args(argv)
@@ -214,7 +216,7 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=dev)
 
     from channelestimationtransformer_amd.dataset import make_batch
-    from channelestimationtransformer_amd.engine import nmse_split
+    from channelestimationtransformer_amd.engine import nmse_split, nmse_split_sums
     from channelestimationtransformer_amd.flops import informer_flops, io_bytes
 
     model = build_model(dev)
@@ -234,7 +236,11 @@ def main(argv=None):
 
     def step(k):
         # forward + NMSE_Split of the batch: one launch (v4 fuses the reduction into its epilogue)
-        eng.forward_nmse(xe, xd, out, lab, None, sums[k] if k >= 0 else warm_sums, stream)
+        if args.nmse == "fused":
+            eng.forward_nmse(xe, xd, out, lab, None, sums[k] if k >= 0 else warm_sums, stream)
+        else:
+            eng.forward(xe, xd, out, None, stream)
+            nmse_split_sums(out, lab, sums[k] if k >= 0 else warm_sums, stream=stream)
 
     t_w = time.perf_counter()
     n_warm = 0
@@ -248,7 +254,7 @@ def main(argv=None):
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.timing(True)
+    eng.timing(True, every=16)     # HIP events around 1 launch in 16 of the timed region
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k)
@@ -307,7 +313,7 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (seeded Jakes channels, SNR %g dB; seeded synthetic weights)" % args.snr,
             "config": {"workload": WORKLOAD, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "nmse": args.nmse},
             "world": world,
             "backend": "nccl" if world > 1 else None,
             "per_rank_ms_per_step": [round(t / args.steps * 1e3, 4) for t in per_rank],

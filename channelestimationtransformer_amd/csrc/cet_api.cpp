@@ -195,8 +195,11 @@ struct cet_engine {
   unsigned long long* stamps = nullptr;
   std::string dbg_json;
 
-  // kernel timing: hipEvents bracketing each forward kernel launch on the caller's stream
+  // kernel timing: hipEvents bracketing one forward kernel launch in every `timing_every` on the
+  // caller's stream (a sample keeps the events' own cost out of the launches between them)
   bool timing = false;
+  int timing_every = 1;
+  int64_t timing_seen = 0;
   std::vector<hipEvent_t> t_ev;
   size_t t_n = 0;
   int64_t attn_floats = 0;
@@ -1021,6 +1024,7 @@ int build_transformer(cet_engine* e) {
 // Record the "before" event of a timed launch (returns the pair index, or -1).
 int timing_mark(cet_engine* e, hipStream_t st) {
   if (!e->timing) return -1;
+  if (e->timing_seen++ % e->timing_every) return -1;
   if (e->t_n * 2 + 2 > e->t_ev.size()) {
     for (int i = 0; i < 64; ++i) {
       hipEvent_t ev_;
@@ -1463,6 +1467,8 @@ int cet_set_variant(cet_engine* e, int variant) {
 int cet_timing(cet_engine* e, int enable) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   e->timing = enable != 0;
+  e->timing_every = enable > 1 ? enable : 1;
+  e->timing_seen = 0;
   e->t_n = 0;
   return CET_OK;
 }

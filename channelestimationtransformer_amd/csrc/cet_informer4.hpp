@@ -336,7 +336,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       const GemmDesc d = PL.proj;
       const int first_row = Ld - PL.pred_len, co = PL.c_out;
       float* out = a.out + (size_t)b * PL.pred_len * co;
+#ifdef V4_NO_FUSE
+      constexpr bool fuse = false;
+#else
       const bool fuse = a.label != nullptr;   // the launcher guarantees c_out ≤ 16 (one n-tile)
+#endif
       gemm_tiles<PP, 4>(M, d, d.n / 16, nmd, LoadImg<PP>{FIN}, [&](int mt, int n0, f32x4 v) {
         const int lane = lane_op();
         const int m = mt * 16 + (lane & 15);
@@ -382,45 +386,71 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   if (a.ticket) {
     __syncthreads();   // every wave's NMSE partials are written (each waited for its own stores)
     unsigned* tk = reinterpret_cast<unsigned*>(lds + v4_scr(P));
-    unsigned tw = 0;
-    if (w == 0) {
-      if (threadIdx.x == 0) tw = atomicAdd(a.ticket, 1u);   // agent-scope add, value returned
-      tw = __shfl(tw, 0, 64);
-      if (threadIdx.x == 0) *tk = tw;
-      if (tw + 1u == (unsigned)a.B) {
-        // ---- last workgroup: the batch's NMSE_Split from every sequence's partials, summed in a fixed
-        //      order (lane l takes sequences l, l+64, ...; then a fixed butterfly): deterministic
-        if (a.label) {
-          const int T = PL.pred_len, lane = threadIdx.x & 63;
-          for (int t = 0; t < T; ++t) {
-            double se = 0.0, pw = 0.0;
-            for (int s = lane; s < a.B; s += 64) {
-              const unsigned long long u = __hip_atomic_load(
-                  reinterpret_cast<const unsigned long long*>(a.nmse_part + (size_t)s * T + t), __ATOMIC_RELAXED,
-                  __HIP_MEMORY_SCOPE_AGENT);
-              const float2 pr = __builtin_bit_cast(float2, u);
-              se += (double)pr.x;
-              pw += (double)pr.y;
-            }
+    if (threadIdx.x == 0) {
+      const unsigned t = atomicAdd(a.ticket, 1u);   // agent-scope add, value returned
+      if (t + 1u == (unsigned)a.B) atomicExch(a.ticket, 0u);   // re-arm for the next launch
+      *tk = t;
+    }
+    __syncthreads();   // the other waves load after this barrier (the adding wave has its value)
+    const unsigned tw = __builtin_amdgcn_readfirstlane(*tk);
+#ifndef V4_NO_FUSE
+    if (a.label && tw + 1u == (unsigned)a.B) {
+      // ---- last workgroup: the batch's NMSE_Split from every sequence's partials.  Thread i takes
+      //      sequences i, i+512, ... (write-through partials, read with sc1 loads); then a fixed
+      //      butterfly per wave and a fixed order over the waves: deterministic.
+      const int T = PL.pred_len, lane = threadIdx.x & 63;
+      double* red = reinterpret_cast<double*>(lds + v4_ctx(P));   // [NW][2][8]
+      for (int t0 = 0; t0 < T; t0 += 8) {
+        const int nt = T - t0 < 8 ? T - t0 : 8;
+        double se[8], pw[8];
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-              se += __shfl_xor(se, o, 64);
-              pw += __shfl_xor(pw, o, 64);
+        for (int j = 0; j < 8; ++j) se[j] = pw[j] = 0.0;
+        for (int s = threadIdx.x; s < a.B; s += NTHREADS) {
+          const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.nmse_part + (size_t)s * T + t0);
+          unsigned long long u[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nt) u[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nt) {
+              const float2 pr = __builtin_bit_cast(float2, u[j]);
+              se[j] += (double)pr.x;
+              pw[j] += (double)pr.y;
             }
-            if (lane == 0) {
-              if (a.nmse_sums) {
-                a.nmse_sums[t] = se;
-                a.nmse_sums[T + t] = pw;
-              }
-              if (a.nmse_acc) a.nmse_acc[t] += (float)(se / pw);
-            }
-          }
         }
-        if (threadIdx.x == 0) atomicExch(a.ticket, 0u);   // re-arm for the next launch
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) {
+            se[j] += __shfl_xor(se[j], o, 64);
+            pw[j] += __shfl_xor(pw[j], o, 64);
+          }
+        if (lane == 0)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            red[(w * 2 + 0) * 8 + j] = se[j];
+            red[(w * 2 + 1) * 8 + j] = pw[j];
+          }
+        __syncthreads();
+        if ((int)threadIdx.x < nt) {
+          const int j = threadIdx.x;
+          double a0 = 0.0, p0 = 0.0;
+          for (int ww = 0; ww < NW; ++ww) {
+            a0 += red[(ww * 2 + 0) * 8 + j];
+            p0 += red[(ww * 2 + 1) * 8 + j];
+          }
+          if (a.nmse_sums) {
+            a.nmse_sums[t0 + j] = a0;
+            a.nmse_sums[T + t0 + j] = p0;
+          }
+          if (a.nmse_acc) a.nmse_acc[t0 + j] += (float)(a0 / p0);
+        }
+        __syncthreads();
       }
     }
-    __syncthreads();
-    const bool elected = __builtin_amdgcn_readfirstlane(*tk) == 0u;
+#endif
+    const bool elected = tw == 0u;
     __syncthreads();   // every wave has read the ticket before the replay reuses the LDS
     if (elected && a.cnt_next)
       replay_all<NTHREADS>(PL, a.mt_in, a.mt_out, a.cnt_next, lds, a.lds_bytes, reinterpret_cast<uint32_t*>(lds),

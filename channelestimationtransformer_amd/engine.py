@@ -167,8 +167,9 @@ class Engine:
         return {v: k for k, v in self.PRECISIONS.items()}[code]
 
     # ------------------------------------------------------------------ kernel timing
-    def timing(self, enable: bool) -> None:
-        check(lib.cet_timing(self._h, int(enable)), "cet_timing")
+    def timing(self, enable, every: int = 1) -> None:
+        """Bracket one forward kernel launch in every ``every`` with hipEvents (off: enable=False)."""
+        check(lib.cet_timing(self._h, max(1, int(every)) if enable else 0), "cet_timing")
 
     def timing_read(self) -> Tuple[float, int]:
         """(summed kernel milliseconds, launches) since ``timing(True)``."""

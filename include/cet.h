@@ -143,9 +143,9 @@ int cet_get_precision(cet_engine* e);
  * (FullPrecision/InformerModel/attn.py:96-98), which is what on_host = 1 mirrors. */
 int cet_set_sampler(cet_engine* e, int on_host);
 
-/* Kernel timing: when enabled, every cet_forward brackets its kernel launch with a pair of
- * hipEvents on the caller's stream; cet_timing_read() waits for them and returns the summed
- * kernel time and launch count since cet_timing(e, 1). */
+/* Kernel timing: when enabled (enable = N ≥ 1), one cet_forward in every N brackets its kernel launch
+ * with a pair of hipEvents on the caller's stream; cet_timing_read() waits for them and returns the
+ * summed kernel time and the number of bracketed launches since cet_timing(e, N). */
 int cet_timing(cet_engine* e, int enable);
 int cet_timing_read(cet_engine* e, double* total_ms, int64_t* launches);
 
