@@ -224,19 +224,23 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       FINE(l, 4);
       if (has_conv) {
         // ---- ConvLayer (encoder.py:22-28): circular conv, BN(eval) folded, ELU, MaxPool(3,2,1)
+        // The conv's m-tiles are computed in even/odd position order (pairs of tiles), so the pool
+        // is an in-register max with a DPP row rotate.
         const GemmDesc d = ELD.conv;
-        with_nmt(nmt, [&](auto NMT) __attribute__((always_inline)) {
+        with_nmt(nmt + (nmt & 1), [&](auto NMT) __attribute__((always_inline)) {
           constexpr int N_ = decltype(NMT)::value;
-          Res<N_> Cv;
-          const WPre<P, 4> pcv = prefetch_kouter<P, 12, 4>(M, d);
-          gemm_kouter_res<P, 12, 4, N_>(pcv, M, d, LoadCirc3<P>{XB, L},
-                                        [&](int mt, int n0, f32x4 v) __attribute__((always_inline)) {
+          if constexpr (N_ % 2 == 0) {
+            Res<N_> Cv;
+            const WPre<P, 4> pcv = prefetch_kouter<P, 12, 4>(M, d);
+            gemm_kouter_res<P, 12, 4, N_>(pcv, M, d, LoadCirc3EO<P>{XB, L},
+                                          [&](int mt, int n0, f32x4 v) __attribute__((always_inline)) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
-            Cv.v[mt] = v;
-          });
-          FINE(l, 5);
-          maxpool_res<N_>(Cv, L, X);
+              for (int r = 0; r < 4; ++r) v[r] = elu1(v[r]);
+              Cv.v[mt] = v;
+            });
+            FINE(l, 5);
+            maxpool_eo<N_>(Cv, L, X);
+          }
         });
         FINE(l, 6);
         L = ELD.L_out;

@@ -150,7 +150,8 @@ constexpr int v4_ctx_bytes(int P) {
 constexpr int v4_scr(int P) { return v4_ctx(P) + v4_ctx_bytes(P); }
 constexpr int v4_cnt(int P) { return v4_scr(P) + 8 * V2_SCR_FLOATS * 4; }   // multiplicity table, LMAX rows
 constexpr int v4_enc(int P) { return v4_cnt(P) + LMAX * 96; }               // stack output (plan-sized)
-static_assert(LMAX * LN3_STRIDE * 4 <= 8 * V2_SCR_FLOATS * 4, "LN partials fit the scratch they alias");
+static_assert(LMAX * LN3_STRIDE * 4 + LMAX * 8 <= 8 * V2_SCR_FLOATS * 4,
+              "LN partials and row statistics fit the scratch they alias");
 static_assert(v4_ctx(0) % 16 == 0 && v4_scr(0) % 16 == 0 && v4_enc(1) % 16 == 0 && v4_enc(2) % 16 == 0, "16-B");
 
 // LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded

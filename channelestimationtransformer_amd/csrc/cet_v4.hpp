@@ -228,6 +228,23 @@ struct LoadCirc3 {
     return im.ld(r, c);
   }
 };
+// The same conv input with the m-tiles in even/odd position order (for the pooling that follows):
+// tile 2j holds positions 32j + 2c, tile 2j+1 positions 32j + 2c + 1 (c = the tile row).
+template <int P>
+struct LoadCirc3EO {
+  Img<P> im;
+  int L;
+  __device__ __forceinline__ XF<P> operator()(int m, int k0) const {
+    const int mt = m >> 4;
+    const int pos = ((mt >> 1) << 5) + ((m & 15) << 1) + (mt & 1);
+    const int tap = k0 >> 7, c = k0 & 127;
+    int r = pos - 1 + tap;
+    r = r < 0 ? r + L : r;
+    r = r >= L ? r - L : r;
+    r = r >= L ? L - 1 : r;  // padded positions only
+    return im.ld(r, c);
+  }
+};
 // Token-embedding input for output row m = position m + off (EncoderStack window):
 // A[m][tap·C + c] = x[(m + off - 1 + tap) mod L][c], zero past 3·C (C a power of two).  The embedding
 // is never quantised: P here is plain_of<>.
@@ -482,17 +499,21 @@ __device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem&
   for (int mt = 0; mt < NMT; ++mt) epi(mt, n0, c[mt] * sc + bi);
 }
 
-// LayerNorm of the register residual over all 128 features (8 waves × 16): each wave reduces its
-// 16 features per row to (mean_w, M2_w), the 8 pairs meet in LDS, Chan's combination gives the
-// exact row statistics.  Normalised rows go to X and rows < `rows` to the image `out` (and `out2`).
-// torch.nn.LayerNorm (biased var, eps in the sqrt) or, if unbiased_std, the reference Transformer's
-// LayerNormalization.  One workgroup barrier inside; the caller adds one before the image is read.
+// LayerNorm of the register residual over all 128 features (8 waves × 16).
+//   1. each wave reduces its 16 features per row to (mean_w, M2_w) and stores the pair (LDS partials);
+//   2. wave w < nmt combines the 8 pairs of the rows of m-tile w (Chan's combination: the exact row
+//      mean / variance) into (mean, 1/std) per row — once per row, not once per wave;
+//   3. every wave normalises its fragments from those row statistics.
+// Normalised rows go to X and rows < `rows` to the image `out` (and `out2`).  torch.nn.LayerNorm
+// (biased var, eps in the sqrt) or, if unbiased_std, the reference Transformer's LayerNormalization.
+// Two workgroup barriers inside; the caller adds one before the image is read.
 template <int N, class Out, class Out2>
 __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
                                        bool unbiased_std, float* part, const Out& out, const Out2* out2) {
   const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
   const int nb = 16 * w + 4 * g;
-  const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barrier
+  float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
+  const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
@@ -512,20 +533,26 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     }
   }
   __syncthreads();
+  if (w < nmt) {
+    const int m = w * 16 + c;
+    const float* pr = part + m * LN_STRIDE;
+    const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
+    const float mean = 0.125f * (((p0[0] + p0[2]) + (p1[0] + p1[2])) + ((p2[0] + p2[2]) + (p3[0] + p3[2])));
+    const float d0 = p0[0] - mean, d1 = p0[2] - mean, d2 = p1[0] - mean, d3 = p1[2] - mean;
+    const float d4 = p2[0] - mean, d5 = p2[2] - mean, d6 = p3[0] - mean, d7 = p3[2] - mean;
+    const float M2 = (((p0[1] + p0[3]) + (p1[1] + p1[3])) + ((p2[1] + p2[3]) + (p3[1] + p3[3]))) +
+                     16.0f * ((d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3) + (d4 * d4 + d5 * d5 + d6 * d6 + d7 * d7));
+    const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
+                                   : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
+    if (g == 0) *reinterpret_cast<f32x2*>(stats + 2 * m) = f32x2{mean, inv};
+  }
+  __syncthreads();
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       const int m = mt * 16 + c;
-      const float* pr = part + m * LN_STRIDE;
-      const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
-      const float mean = 0.125f * (((p0[0] + p0[2]) + (p1[0] + p1[2])) + ((p2[0] + p2[2]) + (p3[0] + p3[2])));
-      const float d0 = p0[0] - mean, d1 = p0[2] - mean, d2 = p1[0] - mean, d3 = p1[2] - mean;
-      const float d4 = p2[0] - mean, d5 = p2[2] - mean, d6 = p3[0] - mean, d7 = p3[2] - mean;
-      const float M2 = (((p0[1] + p0[3]) + (p1[1] + p1[3])) + ((p2[1] + p2[3]) + (p3[1] + p3[3]))) +
-                       16.0f * ((d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3) + (d4 * d4 + d5 * d5 + d6 * d6 + d7 * d7));
-      const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
-                                     : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
-      X.v[mt] = (X.v[mt] - mean) * inv * g0 + b0;
+      const f32x2 st = *reinterpret_cast<const f32x2*>(stats + 2 * m);
+      X.v[mt] = (X.v[mt] - st[0]) * st[1] * g0 + b0;
       if (m < rows) {
         out.st4(m, nb, X.v[mt]);
         if (out2) out2->st4(m, nb, X.v[mt]);
@@ -604,6 +631,37 @@ __device__ __forceinline__ void maxpool_res(const Res<NIN>& in, int L, Res<MT>& 
       const float vm = c == 0 ? c2 : (c <= 8 ? a2 : b2);  // row 2t'-1
       if (row0 + 1 < L) v = fmaxf(v, v1);
       if (row0 - 1 >= 0) v = fmaxf(v, vm);
+      out.v[j][r] = v;
+    }
+  }
+#pragma unroll
+  for (int j = NOUT; j < MT; ++j) out.v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// MaxPool1d(kernel 3, stride 2, padding 1) over even/odd-ordered tiles (LoadCirc3EO): pooled row
+// t' = 16j + c = max(x[2t'], x[2t'+1], x[2t'-1]) = max(E_j[c], O_j[c], O_j[c-1]) where O_j[c-1] for
+// c = 0 is O_{j-1}[15].  The one-row shift is a DPP row rotate (no LDS, no permute through LDS).
+__device__ __forceinline__ float ror1(float v) {   // lane c of each 16-lane row gets lane (c-1) mod 16
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
+}
+template <int NIN>
+__device__ __forceinline__ void maxpool_eo(const Res<NIN>& in, int L, Res<MT>& out) {
+  static_assert(NIN % 2 == 0, "even/odd tile pairs");
+  constexpr int NOUT = NIN / 2;
+  const int c = lane_op() & 15;
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    const int t = 16 * j + c;
+    const bool has_odd = 2 * t + 1 < L, has_prev = t > 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = in.v[2 * j][r], o = in.v[2 * j + 1][r];
+      const float os = ror1(o);
+      const float ps = j > 0 ? ror1(in.v[2 * j - 1][r]) : NEG_INF;
+      const float m1 = c == 0 ? ps : os;
+      float v = e;
+      if (has_odd) v = fmaxf(v, o);
+      if (has_prev) v = fmaxf(v, m1);
       out.v[j][r] = v;
     }
   }
