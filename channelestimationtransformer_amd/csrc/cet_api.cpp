@@ -1018,6 +1018,9 @@ int build_transformer(cet_engine* e) {
   p.lds_bytes = o;
   p.in_stride = c.src_vocab + 4;
   if (o > 160 * 1024) return fail(CET_E_INVALID, "sequence too long for the LDS-resident Transformer kernel");
+  p.lds4_bytes = v4_enc(0) + al(p.tgt_len * p.in_stride * 4);
+  if (p.src_len > LMAX || p.tgt_len > 48 || LMAX * p.in_stride * 4 > v4_ctx_bytes(0))
+    return fail(CET_E_INVALID, "v4 Transformer layout: sequence lengths out of range");
   return CET_OK;
 }
 
@@ -1271,7 +1274,8 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     a.dbg = e->dbg;
     a.B = B;
     const int tk = timing_mark(e, st);
-    rc = cet_launch_transformer(&a, e->tcfg.d_ff, e->tp.lds_bytes, st);
+    rc = e->variant == 1 ? cet_launch_transformer(&a, e->tcfg.d_ff, e->tp.lds_bytes, st)
+                         : cet_launch_transformer_v4(&a, e->tcfg.d_ff, e->tp.lds4_bytes, st);
     if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
     if (rc) return fail(CET_E_HIP, std::string("transformer launch failed: ") + hipGetErrorString(hipGetLastError()));
     return CET_OK;
@@ -1459,7 +1463,8 @@ int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   if (variant != 1 && variant != 3 && variant != 4) return fail(CET_E_INVALID, "variant must be 1, 3 or 4");
   if (variant != e->variant) e->dirty = true;   // the precision resolution depends on the kernel
-  if (e->kind != 0 && variant != 1) return fail(CET_E_INVALID, "the Transformer engine has one variant");
+  if (e->kind != 0 && variant != 1 && variant != 4)
+    return fail(CET_E_INVALID, "the Transformer engine has variants 4 (default) and 1");
   e->variant = variant;
   return CET_OK;
 }

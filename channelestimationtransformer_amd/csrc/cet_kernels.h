@@ -87,5 +87,6 @@ extern "C" int cet_launch_informer_v4(const cet::InformerArgs* a, int prec, int 
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_nmse_split(const float* pred, const float* label, int B, int T, int F, float* acc,
                                      float* last, int accumulate, double* sums, hipStream_t stream);

@@ -172,6 +172,7 @@ struct TransformerPlan {
   int vts;
   int in_stride;
   int dbg_stride, dbg_emb, dbg_enc_out, dbg_dec_emb, dbg_dec_out;
+  int lds4_bytes;           // v4 structure (cet_transformer4.hip): the fixed v4 regions + staged x_dec
 };
 
 }  // namespace cet

@@ -1,0 +1,219 @@
+// Fused models/Transformer inference forward on the v4 building blocks (cet_v4.hpp): 512-thread
+// workgroups, one residual n-tile and one attention head per wave, the residual stream in registers,
+// two sequences per CU (≤ 80 KB of LDS, ≤ 128 VGPRs).  Replaces the LDS-resident v1 structure.
+//
+// Reference: models/Transformer/model.py:76-87 (Transformer.forward: encode, decode, project),
+// encoder.py:41-69 (EncoderBlock, Encoder + final LayerNormalization), decoder.py:48-72 /
+// :117-179 (DecoderBlock: self-attention with tgt_mask = None, cross-attention, FFN),
+// buildingblocks.py:23-30 (LayerNormalization: alpha·(x-mean)/(std_unbiased + eps) + bias, eps 1e-6),
+// :54-65 (FeedForwardBlock, ReLU), :152-192 (MultiHeadAttentionBlock, bias-free Q/K/V/O),
+// :214-226 (ResidualConnection, pre-LN: x + sublayer(norm(x))), embed.py:50-54 / :98-103.
+//
+// LDS: XB (LN output image) | CTX (attention context / FFN hidden / staged input) | scratch | x_dec.
+// The encoder output (90 rows) lives in CTX during the decoder, whose own 16..48-row images take
+// XB's first 48 rows (LN output) and its rows 48..95 (context / hidden).
+#include "cet_kernels.h"
+#include "cet_v4.hpp"
+
+namespace cet {
+namespace v4 {
+
+template <int N>
+using TIC = std::integral_constant<int, N>;
+
+template <int DFF, bool DIAG>
+__global__ void __launch_bounds__(NTHREADS, 4)
+    transformer_forward_v4(TransformerArgs a, const TransformerPlan* __restrict__ plan) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const TransformerPlan& pl = *plan;
+  constexpr int P = P_BF16;
+  constexpr int RS = Geo<P>::RS;
+  const Mem M{make_rsrc(a.weights), make_rsrc(a.params), 0u};
+  const int b = blockIdx.x;
+  if (b >= a.B) return;
+  const int w = wave_id();
+  const float eps = 1e-6f;   // added to the unbiased std (buildingblocks.py:23-30)
+
+  const Img<P> XB{lds + V4L_XB, 0};
+  const Img<P> CTXI{lds + v4_ctx(P), 0};
+  const Img<P> ENC = CTXI;                                  // decoder phase: the encoder output
+  const Img<P> XBD{lds + V4L_XB, 0};                         // decoder LN output (rows < 48)
+  const Img<P> CTXD{lds + V4L_XB + 48 * RS, 0};              // decoder context / FFN hidden
+  float* LNP = reinterpret_cast<float*>(lds + v4_scr(P));
+  float* SCR = reinterpret_cast<float*>(lds + v4_scr(P)) + w * SCR_FLOATS;
+  float* IN = reinterpret_cast<float*>(lds + v4_ctx(P));   // staged x_enc (aliases CTX)
+  float* XDEC = reinterpret_cast<float*>(lds + v4_enc(P));  // staged x_dec (own region, at entry)
+  float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * pl.dbg_stride : nullptr;
+
+  const int C = pl.C, CSH = C == 8 ? 3 : 4, CS = pl.in_stride, L = pl.src_len, Ld = pl.tgt_len;
+  const int t4 = 4 * (int)threadIdx.x;
+  f32x4 xe4 = {0.f, 0.f, 0.f, 0.f}, xd4 = xe4;
+  if (t4 < L * C) xe4 = *reinterpret_cast<const f32x4*>(a.x_enc + (size_t)b * L * C + t4);
+  if (t4 < Ld * C) xd4 = *reinterpret_cast<const f32x4*>(a.x_dec + (size_t)b * Ld * C + t4);
+  for (int i = threadIdx.x; i < v4_enc(P) / 16; i += NTHREADS) reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  if (t4 < L * C) *reinterpret_cast<f32x4*>(IN + (t4 >> CSH) * CS + (t4 & (C - 1))) = xe4;
+  if (t4 < Ld * C) *reinterpret_cast<f32x4*>(XDEC + (t4 >> CSH) * CS + (t4 & (C - 1))) = xd4;
+  __syncthreads();
+
+  constexpr int FRAGS_PER_TILE4 = 4 * WAVE;
+  // full multi-head attention, one head per wave (no masks: the reference forward passes none)
+  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, const Img<P>& ctx, uint32_t Wq,
+                    uint32_t Wk, uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK) {
+    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    HeadIO<P> io;
+    io.xq = Xq; io.xkv = Xkv; io.ctx = ctx; io.wq = Wq; io.wk = Wk; io.wv = Wv;
+    io.dq = dq; io.dk = dk; io.dv = dv;
+    io.LQ = LQ; io.LK = LK; io.prob = 0; io.causal = 0; io.mix = 0; io.u = LQ;
+    io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = nullptr; io.m_dbg = nullptr; io.st = nullptr;
+    attention_head<P, MQ_, MK_>(io, M, w);
+  };
+  auto part_of = [](GemmDesc d, int off) {
+    if (d.bias != NONE) d.bias += off;
+    if (d.scale != NONE) d.scale += off;
+    return d;
+  };
+
+  // ================================ encode (model.py:27-30)
+  Res<MT> X;
+  const int nmt = (L + 15) >> 4;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) X.v[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    const GemmDesc d = pl.emb_src;
+    gemm_res<P, 2, MT>(M, d, nmt, LoadEmbed<P>{IN, L, CSH, CS, 0}, [&](int mt, int n0, f32x4 y) {
+      const int m = mt * 16 + (lane_op() & 15);
+      const int prow = m < L ? m : L - 1;
+      X.v[mt] = y + pload4(M, pl.pe_src, prow * DMODEL + n0);
+    });
+  }
+  __syncthreads();                       // IN (aliases CTX) fully read
+  if (dbg) dump_res(X, nmt, L, dbg + pl.dbg_emb);
+  for (int l = 0; l < pl.N; ++l) {
+    // x = x + MHA(LN0(x))
+    ln_res<MT, Img<P>, Img<P>, false>(X, nmt, L, M, pl.enc[l].ln0, eps, true, LNP, XB, nullptr);
+    __syncthreads();
+    {
+      const GemmDesc q = pl.enc[l].qkv;
+      auto go = [&](auto NQ) __attribute__((always_inline)) {
+        attend(NQ, NQ, XB, XB, CTXI, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
+               part_of(q, 128), part_of(q, 256), L, L);
+      };
+      switch (nmt) {
+        case 1: go(TIC<1>{}); break;
+        case 2: go(TIC<2>{}); break;
+        case 3: go(TIC<3>{}); break;
+        default: go(TIC<MT>{}); break;
+      }
+    }
+    const WPre<P, 4> po = prefetch_res<P, 4>(M, pl.enc[l].o);
+    __syncthreads();
+    gemm_res<P, 4, MT>(po, nmt, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
+    // x = x + FFN(LN1(x))
+    const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, pl.enc[l].f1, DFF / 16);
+    ln_res<MT, Img<P>, Img<P>, false>(X, nmt, L, M, pl.enc[l].ln1, eps, true, LNP, XB, nullptr);
+    __syncthreads();
+    gemm_tiles1<P, 4>(pf1, DFF / 16, nmt, LoadImg<P>{XB}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      CTXI.st4(mt * 16 + (lane_op() & 15), n0, v);
+    });
+    const WPre<P, DFF / 32> pf2 = prefetch_res<P, DFF / 32>(M, pl.enc[l].f2);
+    __syncthreads();
+    gemm_res<P, DFF / 32, MT>(pf2, nmt, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { X.v[mt] += y; });
+    if (dbg && pl.enc[l].dbg >= 0) dump_res(X, nmt, L, dbg + pl.enc[l].dbg);
+  }
+  // Encoder.norm → the encoder output image (CTX: FFN2, its last reader, is done before the LN barrier)
+  ln_res(X, nmt, L, M, pl.enc_norm, eps, true, LNP, ENC, (const Img<P>*)nullptr);
+  __syncthreads();
+  if (dbg) dump_res(X, nmt, L, dbg + pl.dbg_enc_out);
+
+  // ================================ decode (model.py:32-41), compile-time decoder tile count
+  auto decoder = [&](auto NMDc) __attribute__((always_inline)) {
+    constexpr int NMD = decltype(NMDc)::value;
+    Res<NMD> XD;
+    {
+      const GemmDesc d = pl.emb_tgt;
+      gemm_res_n<P, 2, NMD>(M, d, LoadEmbed<P>{XDEC, Ld, CSH, CS, 0}, [&](int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_op() & 15);
+        const int prow = m < Ld ? m : Ld - 1;
+        XD.v[mt] = y + pload4(M, pl.pe_tgt, prow * DMODEL + n0);
+      });
+    }
+    if (dbg) dump_res(XD, NMD, Ld, dbg + pl.dbg_dec_emb);
+    for (int l = 0; l < pl.N; ++l) {
+      const auto& dl = pl.dec[l];
+      // y = y + SelfMHA(LN0(y))   (tgt_mask = None)
+      ln_res<NMD, Img<P>, Img<P>, false>(XD, NMD, Ld, M, dl.ln0, eps, true, LNP, XBD, nullptr);
+      __syncthreads();
+      {
+        const GemmDesc q = dl.qkv;
+        attend(TIC<NMD>{}, TIC<NMD>{}, XBD, XBD, CTXD, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+               part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld);
+      }
+      const WPre<P, 4> po = prefetch_res<P, 4>(M, dl.o);
+      __syncthreads();
+      gemm_res_n<P, 4, NMD>(po, LoadImg<P>{CTXD}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      // y = y + CrossMHA(LN1(y), enc)
+      ln_res<NMD, Img<P>, Img<P>, false>(XD, NMD, Ld, M, dl.ln1, eps, true, LNP, XBD, nullptr);
+      __syncthreads();
+      {
+        const GemmDesc cq = dl.cq, ckv = dl.ckv;
+        attend(TIC<NMD>{}, TIC<MT>{}, XBD, ENC, CTXD, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+               part_of(ckv, 0), part_of(ckv, 128), Ld, L);
+      }
+      const WPre<P, 4> pco = prefetch_res<P, 4>(M, dl.co);
+      __syncthreads();
+      gemm_res_n<P, 4, NMD>(pco, LoadImg<P>{CTXD}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      // y = y + FFN(LN2(y))
+      const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, dl.f1, DFF / 16);
+      ln_res<NMD, Img<P>, Img<P>, false>(XD, NMD, Ld, M, dl.ln2, eps, true, LNP, XBD, nullptr);
+      __syncthreads();
+      gemm_tiles1<P, 4>(pf1, DFF / 16, NMD, LoadImg<P>{XBD}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        CTXD.st4(mt * 16 + (lane_op() & 15), n0, v);
+      });
+      const WPre<P, DFF / 32> pf2 = prefetch_res<P, DFF / 32>(M, dl.f2);
+      __syncthreads();
+      gemm_res_n<P, DFF / 32, NMD>(pf2, LoadImg<P>{CTXD}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      if (dbg && dl.dbg >= 0) dump_res(XD, NMD, Ld, dbg + dl.dbg);
+    }
+    // Decoder.norm → projection (model.py:36-41)
+    ln_res(XD, NMD, Ld, M, pl.dec_norm, eps, true, LNP, XBD, (const Img<P>*)nullptr);
+    __syncthreads();
+    if (dbg) dump_res(XD, NMD, Ld, dbg + pl.dbg_dec_out);
+    const GemmDesc d = pl.proj;
+    const int first_row = Ld - pl.pred_len, co = pl.c_out;
+    float* out = a.out + (size_t)b * pl.pred_len * co;
+    gemm_tiles<P, 4>(M, d, d.n / 16, NMD, LoadImg<P>{XBD}, [&](int mt, int n0, f32x4 v) {
+      const int m = mt * 16 + (lane_op() & 15);
+      if (m < first_row || m >= Ld) return;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n0 + r < co) out[(m - first_row) * co + n0 + r] = v[r];
+    });
+  };
+  switch ((Ld + 15) >> 4) {
+    case 1: decoder(TIC<1>{}); break;
+    case 2: decoder(TIC<2>{}); break;
+    default: decoder(TIC<3>{}); break;
+  }
+}
+
+}  // namespace v4
+}  // namespace cet
+
+extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
+  using namespace cet;
+  if (a->B <= 0) return 0;
+  using K = void (*)(TransformerArgs, const TransformerPlan*);
+  K kern = nullptr;
+  const bool diag = a->dbg != nullptr;
+  if (dff == 64) kern = diag ? v4::transformer_forward_v4<64, true> : v4::transformer_forward_v4<64, false>;
+  else if (dff == 128) kern = diag ? v4::transformer_forward_v4<128, true> : v4::transformer_forward_v4<128, false>;
+  else return -3;
+  if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
+  hipLaunchKernelGGL(kern, dim3(a->B), dim3(v4::NTHREADS), lds_bytes, stream, *a, a->plan);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -507,7 +507,9 @@ __device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem&
 // Normalised rows go to X and rows < `rows` to the image `out` (and `out2`).  torch.nn.LayerNorm
 // (biased var, eps in the sqrt) or, if unbiased_std, the reference Transformer's LayerNormalization.
 // Two workgroup barriers inside; the caller adds one before the image is read.
-template <int N, class Out, class Out2>
+// INPLACE = false (pre-LN residual blocks, models/Transformer buildingblocks.py:214-226): the
+// normalised rows only go to the image(s); X keeps the residual.
+template <int N, class Out, class Out2, bool INPLACE = true>
 __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
                                        bool unbiased_std, float* part, const Out& out, const Out2* out2) {
   const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
@@ -552,10 +554,11 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     if (mt < nmt) {
       const int m = mt * 16 + c;
       const f32x2 st = *reinterpret_cast<const f32x2*>(stats + 2 * m);
-      X.v[mt] = (X.v[mt] - st[0]) * st[1] * g0 + b0;
+      const f32x4 y = (X.v[mt] - st[0]) * st[1] * g0 + b0;
+      if (INPLACE) X.v[mt] = y;
       if (m < rows) {
-        out.st4(m, nb, X.v[mt]);
-        if (out2) out2->st4(m, nb, X.v[mt]);
+        out.st4(m, nb, y);
+        if (out2) out2->st4(m, nb, y);
       }
     }
   }

@@ -14,13 +14,18 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def test_transformer_matches_reference_fixture():
+@pytest.mark.parametrize("variant", [4, 1])
+@pytest.mark.parametrize("instance", ["production", "diag"])
+def test_transformer_matches_reference_fixture(variant, instance):
+    """C3 through the v4-structure kernel (default) and the LDS-resident v1 kernel, production and
+    diagnostic instances, against the reference fixture (per-stage report on failure)."""
     _gpu()
     from engine_util import model_for, run_engine, stage_report
 
     case = load_case("transformer_c3")
     m = model_for(case)
-    out, dbg, _ = run_engine(m, case.z["x_enc"], case.z["x_dec"], debug=True)
+    m.engine(torch.device("cuda:0")).set_variant(variant)
+    out, dbg, _ = run_engine(m, case.z["x_enc"], case.z["x_dec"], debug=instance == "diag")
     rep, _, _ = stage_report(case, out, dbg)
     assert np.isfinite(out).all()
     assert rel_nmse(out, case.z["out"]) < TOL, rep

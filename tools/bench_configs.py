@@ -1,18 +1,22 @@
-"""Throughput of the other BASELINE configs on one MI355X (the headline C2 line is bench.py).
+"""Throughput + parity of the other BASELINE configs on one MI355X (the headline C2 line is bench.py).
 
-  C3  models/Transformer (build_transformer(16,16,90,5,10,128,3,8,0.05,64)), B=512
-  C5  InformerStackLSQ 8-bit weights (QuantizationStudy/LSQ), B=1024 (bf16 activations)
+  C3    models/Transformer (build_transformer(16,16,90,5,10,128,3,8,0.05,64)), B=512
+  C5    InformerStackLSQ 8-bit weights (QuantizationStudy/LSQ), B=1024: bf16 activations (exact integer
+        grid) and fp8 e4m3 activations on the fp8 MFMA (roofline fraction against the fp8 peak)
   full  FullPrecision InformerStack attn="full", e_layers=[4,3] (the TimingAnalysis shape), B=512
 
-Seeded synthetic weights (the golden-case builders), seeded synthetic channel features resident in
-HBM. Kernel time is the engine's own HIP events on the launch stream; one JSON line per config.
+Seeded synthetic weights, seeded synthetic channel features resident in HBM.  Kernel time: the
+engine's HIP events around one launch in 8 (same stream), after a ≥1 s clock-settling warm-up.
+Parity: the same engine with explicit ProbSparse draws on 16 sequences of the batch against the
+float64 oracle (rel-NMSE).  One JSON line per config.
 
-    python tools/bench_configs.py [--steps 100]
+    python tools/bench_configs.py [--steps 200] [--only C5]
 """
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -20,13 +24,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+from channelestimationtransformer_amd.dataset import make_batch  # noqa: E402
 from channelestimationtransformer_amd.flops import informer_flops, transformer_flops  # noqa: E402
 from channelestimationtransformer_amd.informer import InformerStack, InformerStackLSQ  # noqa: E402
-from channelestimationtransformer_amd.spec import informer_stack_spec, transformer_spec  # noqa: E402
+from channelestimationtransformer_amd.rng import draw_indices  # noqa: E402
+from channelestimationtransformer_amd.spec import transformer_spec  # noqa: E402
 from channelestimationtransformer_amd.transformer import build_transformer  # noqa: E402
 from channelestimationtransformer_amd.weights import synthetic_state_dict  # noqa: E402
+from oracle.informer_np import InformerConfig, InformerOracle, sample_shapes  # noqa: E402
+from oracle.transformer_np import TransformerConfig, TransformerOracle  # noqa: E402
 
-PEAK = 2500.0
+PEAK = {"bf16": 2500.0, "fp8": 5000.0}   # dense MFMA TFLOP/s (MI355X_MICROARCH.md chip table)
 
 
 def informer(dev, e_layers, attn, lsq_bits=0):
@@ -37,29 +45,40 @@ def informer(dev, e_layers, attn, lsq_bits=0):
                       strict=False)
     if lsq_bits:
         m.enable_lsq(lsq_bits)
-    return m.eval()
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    orc = InformerOracle(InformerConfig(e_layers=tuple(e_layers), attn=attn, lsq_bits=lsq_bits or None), state)
+    return m.eval(), orc
 
 
 def transformer(dev):
     m = build_transformer(16, 16, 90, 5, 10, 128, 3, 8, 0.05, 64)
     spec = transformer_spec(16, 16, 90, 5, 10, 128, 3, 8, 64)
-    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(spec, 0).items()},
-                      strict=False)
-    return m.eval()
+    state = synthetic_state_dict(spec, 0)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()}, strict=False)
+    return m.eval(), TransformerOracle(TransformerConfig(), state)
 
 
-def time_engine(m, dev, B, steps, warmup=10):
+def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0):
     eng = m.engine(dev)
-    g = torch.Generator().manual_seed(7)
-    xe = (torch.randn(B, 90, 16, generator=g) / 2 ** 0.5).to(dev)
-    xd = torch.cat([xe[:, -10:], torch.zeros(B, 5, 16, device=dev)], 1).contiguous()
+    if variant is not None:
+        eng.set_variant(variant)
+    if precision is not None:
+        eng.set_precision(precision)
+    xe_np, xd_np, _ = make_batch(B, seed=7)
+    xe, xd = torch.from_numpy(xe_np).to(dev), torch.from_numpy(xd_np).to(dev)
     out = torch.empty(B, 5, 16, device=dev)
-    if hasattr(eng, "seed") and eng.prob_calls():
+    prob = bool(eng.prob_calls())
+    if prob:
         eng.seed(1)
-    for _ in range(warmup):
+    t0 = time.perf_counter()
+    n = 0
+    while n < 20 or time.perf_counter() - t0 < settle_s:
         eng.forward(xe, xd, out)
+        n += 1
+        if n % 64 == 0:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
-    eng.timing(True)
+    eng.timing(True, every=8)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(steps):
@@ -69,32 +88,51 @@ def time_engine(m, dev, B, steps, warmup=10):
     ms, k = eng.timing_read()
     eng.timing(False)
     assert torch.isfinite(out).all()
-    return ev0.elapsed_time(ev1) / steps, ms / max(k, 1)
+    # parity of this engine (explicit draws) on 16 sequences of the batch
+    idx = draw_indices(sample_shapes(orc.cfg), seed=3) if prob else None
+    if prob:
+        eng.set_indices(idx)
+    o16 = torch.empty(16, 5, 16, device=dev)
+    eng.forward(xe[:16].contiguous(), xd[:16].contiguous(), o16)
+    torch.cuda.synchronize(dev)
+    if isinstance(orc, InformerOracle):
+        ref = orc.forward(xe_np[:16], xd_np[:16], idx if prob else ())[0]
+    else:
+        ref = orc.forward(xe_np[:16], xd_np[:16])
+    a = o16.cpu().numpy().astype(np.float64)
+    parity = float(np.sum((a - ref) ** 2) / np.sum(ref ** 2))
+    prec = eng.precision() if hasattr(eng, "precision") and eng.kind == "informer" else "bf16"
+    return ev0.elapsed_time(ev1) / steps, ms / max(k, 1), parity, prec
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--only", default="", help="run only the configs whose name contains this")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     runs = [
-        ("C3 Transformer (full attention, no distil), N=3", lambda: transformer(dev), 512, transformer_flops()),
-        ("C5 InformerStackLSQ 8-bit weights, prob+distil, e_layers=[4]", lambda: informer(dev, [4], "prob", 8), 1024,
-         informer_flops()),
+        ("C3 Transformer (full attention, no distil), N=3", lambda: transformer(dev), 512, transformer_flops(),
+         dict(variant=4), "bf16"),
+        ("C3 Transformer, v1 LDS-resident kernel", lambda: transformer(dev), 512, transformer_flops(),
+         dict(variant=1), "bf16"),
+        ("C5 InformerStackLSQ 8-bit weights, bf16 activations", lambda: informer(dev, [4], "prob", 8), 1024,
+         informer_flops(), dict(precision="bf16"), "bf16"),
+        ("C5 InformerStackLSQ 8-bit weights, fp8 e4m3 activations", lambda: informer(dev, [4], "prob", 8), 1024,
+         informer_flops(), dict(precision="fp8"), "fp8"),
         ("FullPrecision InformerStack attn=full, e_layers=[4,3]", lambda: informer(dev, [4, 3], "full"), 512,
-         informer_flops(e_layers=(4, 3), attn="full")),
+         informer_flops(e_layers=(4, 3), attn="full"), {}, "bf16"),
     ]
-    for name, mk, B, flops in runs:
+    for name, mk, B, flops, kw, peak in runs:
         if args.only not in name:
             continue
-        m = mk()
-        step_ms, kern_ms = time_engine(m, dev, B, args.steps)
+        m, orc = mk()
+        step_ms, kern_ms, parity, prec = run(m, orc, dev, B, args.steps, **kw)
         tf = flops * B / (kern_ms * 1e-3) / 1e12
-        print(json.dumps({"config": name, "batch": B, "seq_per_s": round(B / (step_ms * 1e-3), 1),
+        print(json.dumps({"config": name, "batch": B, "precision": prec, "seq_per_s": round(B / (step_ms * 1e-3), 1),
                           "ms_per_step": round(step_ms, 4), "kernel_ms": round(kern_ms, 4),
-                          "flops_per_seq": flops, "tflops": round(tf, 2), "mfma_frac": round(tf / PEAK, 4)}),
-              flush=True)
+                          "flops_per_seq": flops, "tflops": round(tf, 2), "peak_tflops": PEAK[peak],
+                          "mfma_frac": round(tf / PEAK[peak], 4), "parity_rel_nmse_vs_oracle": parity}), flush=True)
 
 
 if __name__ == "__main__":
