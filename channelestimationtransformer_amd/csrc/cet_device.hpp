@@ -93,7 +93,30 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// erf on [-4, 4] (±1 beyond, as in fp32) as an odd/even rational in x²: branch-free, one reciprocal;
+// |error| ≤ 4.2e-7 against the exact erf (GELU's absolute error ≤ 7e-7; tools/erf_check.py).
+__device__ __forceinline__ float erf_rational(float a) {
+  const float x = __builtin_amdgcn_fmed3f(a, -4.0f, 4.0f);
+  const float x2 = x * x;
+  float p = fmaf(x2, -2.72614225801306e-10f, 2.77068142495902e-08f);
+  p = fmaf(p, x2, -2.10102402082508e-06f);
+  p = fmaf(p, x2, -5.69250639462346e-05f);
+  p = fmaf(p, x2, -7.34990630326855e-04f);
+  p = fmaf(p, x2, -2.95459980854025e-03f);
+  p = fmaf(p, x2, -1.60960333262415e-02f);
+  float q = fmaf(x2, -1.45660718464996e-05f, -2.13374055278905e-04f);
+  q = fmaf(q, x2, -1.68282697438203e-03f);
+  q = fmaf(q, x2, -7.37332916720468e-03f);
+  q = fmaf(q, x2, -1.42647390514189e-02f);
+  return x * p * __builtin_amdgcn_rcpf(q);
+}
+#if defined(CET_ABL_GELU)
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x; }   // ablation (wrong results)
+#elif defined(CET_OCML_ERF)
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+#else
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_rational(x * 0.70710678118654752f)); }
+#endif
 // exp(x) - 1 on v_exp_f32: absolute error ~1e-7 near 0, far inside the parity bar
 __device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : __expf(x) - 1.0f; }
 

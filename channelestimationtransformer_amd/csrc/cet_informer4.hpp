@@ -61,6 +61,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   const int b = blockIdx.x;
   if (b >= a.B) return;
   const int w = wave_id();
+#ifndef CET_NO_SETPRIO
+  // static priority for the younger half of the workgroup, the SIMD arbitration loser
+  // (MI355X_MICROARCH "Two waves per SIMD" item 4): −0.7 µs at C2 (profiles/r02/ab_erf_setprio.log)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 
   const Img<P> XB{lds + V4L_XB, G::IMG};
   const Img<P> CTXI{lds + v4_ctx(P), G::IMG};                           // attention context / FFN hidden
@@ -141,8 +146,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         const int bytes = ((c.LQ + 15) & ~15) * c.cnt_stride;
         const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + c.cnt_off);
         f32x4* dst = reinterpret_cast<f32x4*>(CNT);
+#ifndef CET_ABL_CNT
         for (int i = threadIdx.x; i < bytes / 16; i += NTHREADS) dst[i] = src[i];
         __syncthreads();
+#else
+        (void)bytes; (void)src; (void)dst;   // ablation (wrong results)
+#endif
       }
       if (sparse) io.cnt = CNT;
     }
@@ -289,7 +298,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_emb);
     STAMP();  // decoder embedding
 
+#ifdef CET_ABL_DEC
+    for (int l = 0; l < 0; ++l) {   // ablation (wrong results)
+#else
     for (int l = 0; l < PL.d_layers; ++l) {
+#endif
       {
         // masked self-attention with the mix scramble (model.py:211-222)
         const GemmDesc q = DLD.qkv;

@@ -518,7 +518,11 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
+#ifdef CET_ABL_LN
+    if (false) {
+#else
     if (mt < nmt) {
+#endif
       float s = (X.v[mt][0] + X.v[mt][1]) + (X.v[mt][2] + X.v[mt][3]);
       s = xor_sum(s, 16);
       s = xor_sum(s, 32);
@@ -535,7 +539,11 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     }
   }
   __syncthreads();
+#ifdef CET_ABL_LN
+  if (w < 0) {
+#else
   if (w < nmt) {
+#endif
     const int m = w * 16 + c;
     const float* pr = part + m * LN_STRIDE;
     const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
@@ -771,9 +779,14 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
           const uint32_t cw = cws[kt];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
+#ifdef CET_ABL_MVALU
+            sum += s[r]; (void)cw;   // ablation (wrong results)
+            mx = fmaxf(mx, s[r]);
+#else
             const float cf = (float)((cw >> (8 * r)) & 0xffu);
             sum = fmaf(cf, s[r], sum);
             mx = fmaxf(mx, cf != 0.f ? s[r] : NEG_INF);
+#endif
           }
         }
       }
@@ -804,8 +817,13 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
     }
     const int J = 4 * nqt;
     const uint64_t* kg = keys + g * J;
+#ifdef CET_ABL_TOPU
+    for (int qt = 0; qt < MQ; ++qt) rank[qt] = g == 0 ? qt * 16 + col : 0;   // ablation (wrong results)
+    for (int j = 0; j < 0; j += 2) {
+#else
 #pragma unroll 2
     for (int j = 0; j < J; j += 2) {
+#endif
       const u64x2 kk = *reinterpret_cast<const u64x2*>(kg + j);
 #pragma unroll
       for (int qt = 0; qt < MQ; ++qt) rank[qt] += (int)(kk[0] > myk[qt]) + (int)(kk[1] > myk[qt]);
