@@ -17,6 +17,7 @@
 
 #include "../../include/cet.h"
 #include "cet_kernels.h"
+#include "cet_lw.h"
 #include "cet_plan.hpp"
 
 using namespace cet;
@@ -134,6 +135,11 @@ struct cet_engine {
   bool dirty = true;
   bool uploaded = false;
   int variant = 4;   // fused-kernel generation (CET_KERNEL=v1 / v3 select the older kernels)
+  // shapes outside the fused kernels (d_model != 128, n_heads != 8, d_ff > 128, ...): the layer-wise
+  // engine (cet_lw.hip), fp32 on the f32 MFMA, one launch per operator
+  bool generic = false;
+  std::unique_ptr<cet::lw::Model> lw;
+  int32_t* h_lwidx[4] = {};   // pinned staging of each forward's draws (ring, events ev[])
 
   // packed blobs
   std::vector<uint16_t> wblob;
@@ -221,6 +227,8 @@ struct cet_engine {
     if (d_ticket) (void)hipFree(d_ticket);
     if (d_nmse_part) (void)hipFree(d_nmse_part);
     if (h_mt) (void)hipHostFree(h_mt);
+    for (auto* h : h_lwidx)
+      if (h) (void)hipHostFree(h);
     if (ev_mt) (void)hipEventDestroy(ev_mt);
   }
 
@@ -252,10 +260,14 @@ void schema_embedding(cet_engine* e, const std::string& p, int c_in, int d) {
   for (int i = 0; i < 4; ++i) e->add(p + ".temporal_embedding." + names[i] + ".emb.weight", {rows[i], d}, false);
 }
 
-void schema_attn(cet_engine* e, const std::string& p, int d, bool lsq) {
+// AttentionLayer (attn.py:178-193): d_keys = d_values = d_model // n_heads; q/k/v project d_model →
+// d_keys·n_heads, out projects d_values·n_heads → d_model
+void schema_attn(cet_engine* e, const std::string& p, int d, int heads, bool lsq) {
+  const int he = (d / heads) * heads;
   for (const char* n : {"query_projection", "key_projection", "value_projection", "out_projection"}) {
-    e->add(p + "." + n + ".weight", {d, d});
-    e->add(p + "." + n + ".bias", {d});
+    const bool out = std::strcmp(n, "out_projection") == 0;
+    e->add(p + "." + n + ".weight", {out ? d : he, out ? he : d});
+    e->add(p + "." + n + ".bias", {out ? d : he});
     if (lsq) e->add(p + "." + n + ".step_size", {});
   }
 }
@@ -284,7 +296,7 @@ void schema_informer(cet_engine* e) {
     const std::string pre = c.stack ? "encoder.encoders." + std::to_string(i) : std::string("encoder");
     for (int l = 0; l < c.e_layers[i]; ++l) {
       const std::string p = pre + ".attn_layers." + std::to_string(l);
-      schema_attn(e, p + ".attention", d, lsq);
+      schema_attn(e, p + ".attention", d, c.n_heads, lsq);
       schema_ffn(e, p, d, c.d_ff, lsq);
       schema_ln(e, p + ".norm1", d);
       schema_ln(e, p + ".norm2", d);
@@ -305,8 +317,8 @@ void schema_informer(cet_engine* e) {
   }
   for (int l = 0; l < c.d_layers; ++l) {
     const std::string p = "decoder.layers." + std::to_string(l);
-    schema_attn(e, p + ".self_attention", d, lsq);
-    schema_attn(e, p + ".cross_attention", d, lsq);
+    schema_attn(e, p + ".self_attention", d, c.n_heads, lsq);
+    schema_attn(e, p + ".cross_attention", d, c.n_heads, lsq);
     schema_ffn(e, p, d, c.d_ff, lsq);
     schema_ln(e, p + ".norm1", d);
     schema_ln(e, p + ".norm2", d);
@@ -481,7 +493,10 @@ int resolve_precision(cet_engine* e, float qmax, int* out) {
   return CET_OK;
 }
 
+int build_lw(cet_engine* e);
+
 int build_informer(cet_engine* e) {
+  if (e->generic) return build_lw(e);
   const auto& c = e->icfg;
   const int D = c.d_model;
   auto& wb = e->wblob;
@@ -796,17 +811,205 @@ int build_informer(cet_engine* e) {
   return CET_OK;
 }
 
+// The layer-wise model (cet_lw.h): weights as fp32 [N][K] matrices — LSQ grids fake-quantised on the
+// host exactly as LSQ.py:65-74 (w_q = round_half_even(clamp(w/s, Qn, Qp))·s), BatchNorm(eval) of the
+// distil ConvLayer folded into a per-channel scale / shift, conv kernels reordered to [n][tap·C + c].
+int build_lw(cet_engine* e) {
+  const auto& c = e->icfg;
+  auto m = std::make_unique<lw::Model>();
+  const int D = c.d_model, H = c.n_heads, E = D / H, HE = E * H;
+  const bool lsq = c.lsq_bits > 0;
+  m->C = c.enc_in;
+  m->Cd = c.dec_in;
+  m->c_out = c.c_out;
+  m->L0 = c.seq_len;
+  m->Ld = c.label_len + c.out_len;
+  m->pred = c.out_len;
+  m->D = D;
+  m->H = H;
+  m->E = E;
+  m->HE = HE;
+  m->dff = c.d_ff;
+  m->prob = c.attn_prob;
+  m->mix = c.mix;
+  m->act = c.act_relu ? 2 : 1;
+  m->stack = c.stack;
+  m->out_attn = c.output_attention;
+  e->prec = 3;
+  auto Wq = [&](const std::string& n) {   // a quantisable module's weight, LSQ applied
+    std::vector<float> w = e->W(n + ".weight");
+    if (lsq && e->has(n + ".step_size")) {
+      const float st = e->scalar(n + ".step_size");
+      (void)lsq_grid(w, st, c.lsq_bits);
+      for (auto& x : w) x *= st;
+    }
+    return w;
+  };
+  auto dense = [&](std::vector<std::string> names, size_t& w, size_t& b) {
+    std::vector<float> ww, bb;
+    for (auto& n : names) {
+      const auto wi = Wq(n);
+      ww.insert(ww.end(), wi.begin(), wi.end());
+      const auto& bi = e->W(n + ".bias");
+      bb.insert(bb.end(), bi.begin(), bi.end());
+    }
+    w = m->push(ww);
+    b = m->push(bb);
+  };
+  auto conv3 = [&](const std::vector<float>& w, int N, int Cin) {   // [n][c][tap] → [n][tap·Cin + c]
+    std::vector<float> r((size_t)N * 3 * Cin);
+    for (int n = 0; n < N; ++n)
+      for (int ch = 0; ch < Cin; ++ch)
+        for (int tap = 0; tap < 3; ++tap) r[(size_t)n * 3 * Cin + tap * Cin + ch] = w[((size_t)n * Cin + ch) * 3 + tap];
+    return r;
+  };
+  auto vec = [&](const std::string& n) { return m->push(e->W(n)); };
+  auto pe_rows = [&](const std::string& n, int L) {
+    const auto& pe = e->W(n);
+    return m->push(std::vector<float>(pe.begin(), pe.begin() + (size_t)L * D));
+  };
+  m->emb_enc_w = m->push(conv3(e->W("enc_embedding.value_embedding.tokenConv.weight"), D, c.enc_in));
+  m->emb_enc_b = vec("enc_embedding.value_embedding.tokenConv.bias");
+  m->pe_enc = pe_rows("enc_embedding.position_embedding.pe", c.seq_len);
+  m->emb_dec_w = m->push(conv3(e->W("dec_embedding.value_embedding.tokenConv.weight"), D, c.dec_in));
+  m->emb_dec_b = vec("dec_embedding.value_embedding.tokenConv.bias");
+  m->pe_dec = pe_rows("dec_embedding.position_embedding.pe", m->Ld);
+  int call = 0, S = 0;
+  int64_t attn_off = 0;
+  e->attn_layout.clear();
+  for (int i = 0; i < c.n_enc; ++i) {
+    const std::string pre = c.stack ? "encoder.encoders." + std::to_string(i) : std::string("encoder");
+    int L = c.stack ? (c.seq_len >> i) : c.seq_len;   // inp_len = x.shape[1] // 2**i (encoder.py:102)
+    m->enc_L0.push_back(L);
+    std::vector<lw::EncLayer> layers;
+    for (int l = 0; l < c.e_layers[i]; ++l) {
+      lw::EncLayer d{};
+      const std::string lp = pre + ".attn_layers." + std::to_string(l);
+      dense({lp + ".attention.query_projection", lp + ".attention.key_projection", lp + ".attention.value_projection"},
+            d.wqkv, d.bqkv);
+      dense({lp + ".attention.out_projection"}, d.wo, d.bo);
+      dense({lp + ".conv1"}, d.w1, d.b1);
+      dense({lp + ".conv2"}, d.w2, d.b2);
+      d.g1 = vec(lp + ".norm1.weight");
+      d.be1 = vec(lp + ".norm1.bias");
+      d.g2 = vec(lp + ".norm2.weight");
+      d.be2 = vec(lp + ".norm2.bias");
+      d.L_in = L;
+      d.call = c.attn_prob ? call++ : -1;
+      d.attn_off = attn_off;
+      if (c.output_attention) {
+        e->attn_layout.push_back({attn_off, L});
+        attn_off += (int64_t)H * L * L;
+      }
+      d.conv = c.distil && l < c.e_layers[i] - 1;
+      d.L_out = L;
+      if (d.conv) {
+        const std::string cp = pre + ".conv_layers." + std::to_string(l);
+        float step = 1.f;
+        std::vector<float> w = e->W(cp + ".downConv.weight");
+        if (lsq && e->has(cp + ".downConv.step_size")) {
+          step = e->scalar(cp + ".downConv.step_size");
+          (void)lsq_grid(w, step, c.lsq_bits);   // the integer grid; the step joins the BN scale
+        }
+        d.wc = m->push(conv3(w, D, D));
+        const auto& cb = e->W(cp + ".downConv.bias");
+        const auto& g = e->W(cp + ".norm.weight");
+        const auto& bb = e->W(cp + ".norm.bias");
+        const auto& rm = e->W(cp + ".norm.running_mean");
+        const auto& rv = e->W(cp + ".norm.running_var");
+        std::vector<float> sc(D), sh(D);
+        for (int n = 0; n < D; ++n) {
+          const double inv = (double)g[n] / std::sqrt((double)rv[n] + 1e-5);
+          sc[n] = (float)(inv * step);
+          sh[n] = (float)(((double)cb[n] - rm[n]) * inv + bb[n]);
+        }
+        d.sc = m->push(sc);
+        d.sh = m->push(sh);
+        d.L_out = (L - 1) / 2 + 1;
+        L = d.L_out;
+      }
+      layers.push_back(d);
+    }
+    m->enc.push_back(layers);
+    m->norm_g.push_back(vec(pre + ".norm.weight"));
+    m->norm_b.push_back(vec(pre + ".norm.bias"));
+    m->enc_rows.push_back(L);
+    m->enc_off.push_back(S);
+    S += L;
+  }
+  m->S = S;
+  for (int l = 0; l < c.d_layers; ++l) {
+    lw::DecLayer d{};
+    const std::string lp = "decoder.layers." + std::to_string(l);
+    dense({lp + ".self_attention.query_projection", lp + ".self_attention.key_projection",
+           lp + ".self_attention.value_projection"}, d.wqkv, d.bqkv);
+    dense({lp + ".self_attention.out_projection"}, d.wo, d.bo);
+    dense({lp + ".cross_attention.query_projection"}, d.wcq, d.bcq);
+    dense({lp + ".cross_attention.key_projection", lp + ".cross_attention.value_projection"}, d.wckv, d.bckv);
+    dense({lp + ".cross_attention.out_projection"}, d.wco, d.bco);
+    dense({lp + ".conv1"}, d.w1, d.b1);
+    dense({lp + ".conv2"}, d.w2, d.b2);
+    d.g1 = vec(lp + ".norm1.weight");
+    d.be1 = vec(lp + ".norm1.bias");
+    d.g2 = vec(lp + ".norm2.weight");
+    d.be2 = vec(lp + ".norm2.bias");
+    d.g3 = vec(lp + ".norm3.weight");
+    d.be3 = vec(lp + ".norm3.bias");
+    d.call = c.attn_prob ? call++ : -1;
+    m->dec.push_back(d);
+  }
+  m->dnorm_g = vec("decoder.norm.weight");
+  m->dnorm_b = vec("decoder.norm.bias");
+  m->proj_w = vec("projection.weight");
+  m->proj_b = vec("projection.bias");
+  size_t off = 0;
+  for (const auto& cl : e->calls) {
+    m->call_LQ.push_back(cl.LQ);
+    m->call_LK.push_back(cl.LK);
+    m->call_U.push_back(cl.U);
+    m->call_u.push_back(u_part(c.factor, cl.LQ));
+    m->idx_off.push_back(off);
+    off += (size_t)cl.LQ * cl.U;
+  }
+  m->idx_total = off;
+  m->attn_floats = attn_off;
+  e->attn_floats = attn_off;
+  e->dbg_json = "{\"stages\": [], \"m\": []}";
+  std::memset(&e->ip, 0, sizeof(e->ip));
+  e->ip.n_calls = (int)e->calls.size();
+  e->lw = std::move(m);
+  return CET_OK;
+}
+
 int build_transformer(cet_engine* e);
 
-int check_informer_config(const cet_informer_config& c) {
-  if (c.d_model != DMODEL || c.n_heads != NHEAD)
-    return fail(CET_E_INVALID, "this build supports d_model=128, n_heads=8 (head dim 16)");
-  if (c.enc_in != c.dec_in || (c.enc_in != 8 && c.enc_in != 16))
-    return fail(CET_E_INVALID, "enc_in == dec_in in {8, 16} required");
-  if (c.d_ff != 64 && c.d_ff != 128) return fail(CET_E_INVALID, "d_ff must be 64 or 128 in this build");
-  if (c.seq_len < 2 || c.seq_len > LMAX) return fail(CET_E_INVALID, "seq_len must be in [2, 96]");
+// Can the fused kernels (d_model 128, 8 heads of 16, d_ff 64 / 128, ≤ 96 rows) carry the model?
+bool fused_supported(const cet_informer_config& c) {
+  if (c.d_model != DMODEL || c.n_heads != NHEAD) return false;
+  if (c.enc_in != c.dec_in || (c.enc_in != 8 && c.enc_in != 16)) return false;
+  if (c.d_ff != 64 && c.d_ff != 128) return false;
+  if (c.seq_len < 2 || c.seq_len > LMAX) return false;
   const int Ld = c.label_len + c.out_len;
-  if (Ld < 1 || Ld > 48 || c.out_len < 1 || c.out_len > Ld) return fail(CET_E_INVALID, "label_len+out_len must be in [1, 48]");
+  if (Ld > 48) return false;
+  int S = 0;
+  for (int i = 0; i < c.n_enc && i < MAX_ENC; ++i) {
+    int L = c.stack ? (c.seq_len >> i) : c.seq_len;
+    for (int l = 0; l < c.e_layers[i] - 1; ++l)
+      if (c.distil) L = (L - 1) / 2 + 1;
+    S += L;
+  }
+  return S <= LMAX && c.c_out <= 128;
+}
+
+int check_informer_config(const cet_informer_config& c) {
+  if (c.d_model < 1 || c.d_model > lw::LW_DMAX) return fail(CET_E_INVALID, "d_model must be in [1, 1024]");
+  if (c.n_heads < 1 || c.n_heads > c.d_model) return fail(CET_E_INVALID, "n_heads must be in [1, d_model]");
+  if (c.enc_in < 1 || c.dec_in < 1 || c.enc_in > 1024 || c.dec_in > 1024) return fail(CET_E_INVALID, "enc_in / dec_in out of range");
+  if (c.d_ff < 1 || c.d_ff > 8192) return fail(CET_E_INVALID, "d_ff must be in [1, 8192]");
+  if (c.seq_len < 2 || c.seq_len > lw::LW_LMAX) return fail(CET_E_INVALID, "seq_len must be in [2, 128]");
+  const int Ld = c.label_len + c.out_len;
+  if (Ld < 1 || Ld > lw::LW_LMAX || c.out_len < 1 || c.out_len > Ld)
+    return fail(CET_E_INVALID, "label_len+out_len must be in [1, 128]");
   if (c.n_enc < 1 || c.n_enc > MAX_ENC) return fail(CET_E_INVALID, "1..4 encoders");
   if (!c.stack && c.n_enc != 1) return fail(CET_E_INVALID, "Informer has one encoder");
   int S = 0, layers = 0;
@@ -820,15 +1023,27 @@ int check_informer_config(const cet_informer_config& c) {
     S += L;
   }
   if (layers > MAX_ENC_LAYERS) return fail(CET_E_INVALID, "too many encoder layers");
-  if (S > LMAX) return fail(CET_E_INVALID, "encoder stack output longer than 96 rows");
+  if (S > lw::LW_LMAX) return fail(CET_E_INVALID, "encoder stack output longer than 128 rows");
   if (c.d_layers < 1 || c.d_layers > MAX_DEC_LAYERS) return fail(CET_E_INVALID, "1..8 decoder layers");
-  if (c.c_out < 1 || c.c_out > 128) return fail(CET_E_INVALID, "c_out must be in [1, 128]");
+  if (c.c_out < 1 || c.c_out > 1024) return fail(CET_E_INVALID, "c_out must be in [1, 1024]");
   if (c.factor < 1) return fail(CET_E_INVALID, "factor must be >= 1");
   if (c.lsq_bits < 0 || c.lsq_bits == 1 || c.lsq_bits > 16) return fail(CET_E_INVALID, "lsq_bits must be 0 or 2..16");
   return CET_OK;
 }
 
 int upload(cet_engine* e) {
+  if (e->kind == 0 && e->generic) {
+    if (e->lw->upload()) return fail(CET_E_HIP, "layer-wise weight upload failed");
+    for (auto*& h : e->h_lwidx) {
+      if (h) HIP_TRY(hipHostFree(h));
+      HIP_TRY(hipHostMalloc((void**)&h, std::max<size_t>(e->lw->idx_total, 1) * sizeof(int32_t)));
+    }
+    for (int i = 0; i < cet_engine::NSLOT; ++i) {
+      if (!e->ev[i]) HIP_TRY(hipEventCreateWithFlags(&e->ev[i], hipEventDisableTiming));
+      e->ev_used[i] = false;
+    }
+    return CET_OK;
+  }
   const void* plan = e->kind == 0 ? (const void*)&e->ip : (const void*)&e->tp;
   const size_t plan_bytes = e->kind == 0 ? sizeof(InformerPlan) : sizeof(TransformerPlan);
   if (!e->d_plan) HIP_TRY(hipMalloc(&e->d_plan, sizeof(InformerPlan) > sizeof(TransformerPlan)
@@ -1055,6 +1270,7 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   auto e = std::make_unique<cet_engine>();
   e->kind = 0;
   e->icfg = *cfg;
+  e->generic = !fused_supported(*cfg) || std::getenv("CET_LAYERWISE") != nullptr;
   if (const char* v = std::getenv("CET_KERNEL"))
     e->variant = std::strcmp(v, "v1") == 0 ? 1 : (std::strcmp(v, "v3") == 0 ? 3 : 4);
   schema_informer(e.get());
@@ -1243,6 +1459,54 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
 static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
                         const float* label, float* nmse_acc, double* nmse_sums, void* stream);
 
+// Layer-wise forward: this forward's ProbSparse draws (explicit indices, or the native stream drawn
+// on the host — the same torch.randint sequence) staged through a pinned ring, then the operator
+// launches, then NMSE_Split if a label is given.
+static int forward_lw(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
+                      const float* label, float* nmse_acc, double* nmse_sums, hipStream_t st) {
+  const int n_calls = (int)e->calls.size();
+  bool explicit_idx = n_calls > 0, any_idx = false;
+  for (int c = 0; c < n_calls; ++c) {
+    explicit_idx = explicit_idx && e->idx_set[c];
+    any_idx = any_idx || e->idx_set[c];
+  }
+  if (any_idx && !explicit_idx) return fail(CET_E_STATE, "ProbSparse indices set for some calls only");
+  if (n_calls && !explicit_idx && !e->native_rng)
+    return fail(CET_E_STATE, "ProbSparse indices not set (cet_set_prob_indices for every call, or cet_seed)");
+  if (n_calls) {
+    if (!explicit_idx) {
+      e->sync_host_rng();
+      e->dev_mt_valid = false;
+    }
+    const int k = e->slot;
+    e->slot = (e->slot + 1) % cet_engine::NSLOT;
+    if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
+    int32_t* h = e->h_lwidx[k];
+    size_t o = 0;
+    for (int c = 0; c < n_calls; ++c) {
+      const auto& sh = e->calls[c];
+      const size_t n = (size_t)sh.LQ * sh.U;
+      if (explicit_idx) {
+        std::memcpy(h + o, e->idx[c].data(), n * sizeof(int32_t));
+      } else {
+        for (size_t i = 0; i < n; ++i) h[o + i] = (int32_t)(e->rng.next() % (uint32_t)sh.LK);
+      }
+      o += n;
+    }
+    if (explicit_idx) e->idx_set.assign(e->calls.size(), false);
+    HIP_TRY(hipMemcpyAsync(e->lw->d_idx, h, o * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(e->ev[k], st));
+    e->ev_used[k] = true;
+  }
+  const int tk = timing_mark(e, st);
+  const int rc = e->lw->forward(x_enc, x_dec, B, out, attns, e->lw->d_idx, st);
+  if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
+  if (rc) return fail(CET_E_HIP, std::string("layer-wise launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (label && cet_launch_nmse_split(out, label, B, e->icfg.out_len, e->icfg.c_out, nmse_acc, nullptr, 1, nmse_sums, st))
+    return fail(CET_E_HIP, "nmse launch failed");
+  return CET_OK;
+}
+
 int cet_forward(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
                 void* stream) {
   return forward_impl(e, x_enc, x_dec, B, out, attns, nullptr, nullptr, nullptr, stream);
@@ -1280,6 +1544,7 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     if (rc) return fail(CET_E_HIP, std::string("transformer launch failed: ") + hipGetErrorString(hipGetLastError()));
     return CET_OK;
   }
+  if (e->generic) return forward_lw(e, x_enc, x_dec, B, out, attns, label, nmse_acc, nmse_sums, st);
   const InformerPlan& p = e->ip;
   InformerArgs a;
   a.plan = (const InformerPlan*)e->d_plan;
@@ -1439,6 +1704,8 @@ int cet_set_precision(cet_engine* e, int prec) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   if (e->kind != 0) return fail(CET_E_INVALID, "precision modes are Informer-engine only");
   if (prec < -1 || prec > 2) return fail(CET_E_INVALID, "precision must be -1 (auto), 0 (bf16), 1 (split bf16) or 2 (fp8)");
+  if (e->generic && prec != -1)
+    return fail(CET_E_INVALID, "the layer-wise engine (shapes outside the fused kernels) computes in fp32 only");
   e->prec_req = prec;
   e->dirty = true;
   return CET_OK;

@@ -1,0 +1,114 @@
+// Layer-wise engine (cet_lw.hip, cet_lw_host.cpp): operator argument blocks and launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace cet {
+namespace lw {
+
+constexpr int LW_DMAX = 1024;   // widest LayerNorm row (d_model)
+constexpr int LW_LMAX = 128;    // longest sequence an attention workgroup holds (S in LDS)
+
+// Y[m][n] = epi(Σ_k A(m, k) · W[n][k]),  epi(y) = act(y·scale[n] + bias[n] + pe[t][n]) + R[m][n].
+// Rows are sequence-major: m = b·L + t.  amode 0: A(m, k) = A[m·lda + k]; amode 1: circular k=3
+// conv, A(m, tap·Cin + c) = A[(b·Ls + off + (t − 1 + tap) mod L)·lda + c].  row_t0 > 0 keeps only
+// rows t ≥ row_t0, written densely as Y[b][t − row_t0].  act: 0 none, 1 GELU (erf), 2 ReLU, 3 ELU.
+struct GemmOp {
+  int M, N, K;
+  const float* A;
+  int lda, amode, L, Ls, off, Cin;
+  const float* W;      // [N][K]
+  const float* bias;   // [N] or null
+  const float* scale;  // [N] or null
+  const float* pe;     // [L][N] or null
+  int act;
+  const float* R;      // residual [M][ldr] or null (may alias Y)
+  int ldr;
+  float* Y;
+  int ldy;
+  int row_t0;
+};
+
+// LayerNorm of M rows of width D (eps 1e-5, biased variance); input row m = b·L + t goes to output
+// row b·Lo + off + t (Lo = L, off = 0: in place or a plain copy).
+struct LnOp {
+  int M, D, L, Lo, off;
+  const float* X;
+  float* Y;
+  const float* g;
+  const float* b;
+};
+
+// Attention of every (sequence, head): Q rows b·LQ + i at column h·E (row stride ldq), K/V rows
+// b·LK + j.  prob: ProbSparse with the call's draws idx[LQ][U] and u; causal: keys j > i masked
+// (and cumsum(V) as the initial context); mix: the (L, H, E) → (H, L, E) re-view of the output
+// (requires ldo = H·E).  attns: [B][H][LQ][LK] maps or null.
+struct AttnOp {
+  int H, E, LQ, LK;
+  const float* Q;
+  int ldq;
+  const float* K;
+  int ldk;
+  const float* V;
+  int ldv;
+  float* O;
+  int ldo;
+  int prob, causal, mix, U, u;
+  const int32_t* idx;
+  float* attns;            // map of (b, h, i, j) at attns + b·attn_bstride + (h·LQ + i)·LK + j
+  int64_t attn_bstride;
+};
+
+int launch_gemm(const GemmOp& op, hipStream_t st);
+int launch_layernorm(const LnOp& op, hipStream_t st);
+int launch_maxpool(const float* X, float* Y, int B, int L, int Lo, int D, hipStream_t st);
+int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStream_t st);
+int launch_attention(const AttnOp& op, int B, hipStream_t st);
+size_t attn_lds_bytes(int LQ, int LK);
+
+// ------------------------------------------------------------------ host model (cet_lw_host.cpp)
+// Weights as fp32 [N][K] matrices in one device blob (float offsets below); ProbSparse draws of a
+// forward concatenated in call order (call c's [LQ][U] table at idx_off[c]).
+struct EncLayer {
+  size_t wqkv, bqkv, wo, bo, w1, b1, w2, b2, g1, be1, g2, be2;
+  int conv;
+  size_t wc, sc, sh;   // distil conv [D][3D] with BatchNorm(eval) folded into scale / shift
+  int L_in, L_out, call;
+  int64_t attn_off;
+};
+struct DecLayer {
+  size_t wqkv, bqkv, wo, bo, wcq, bcq, wckv, bckv, wco, bco, w1, b1, w2, b2, g1, be1, g2, be2, g3, be3;
+  int call;
+};
+struct Model {
+  int C = 0, Cd = 0, c_out = 0, L0 = 0, Ld = 0, pred = 0, D = 0, H = 0, E = 0, HE = 0, dff = 0, S = 0;
+  int prob = 0, mix = 0, act = 1, stack = 1, out_attn = 0;
+  size_t emb_enc_w = 0, emb_enc_b = 0, pe_enc = 0, emb_dec_w = 0, emb_dec_b = 0, pe_dec = 0;
+  std::vector<std::vector<EncLayer>> enc;
+  std::vector<size_t> norm_g, norm_b;
+  std::vector<int> enc_L0, enc_rows, enc_off;
+  std::vector<DecLayer> dec;
+  size_t dnorm_g = 0, dnorm_b = 0, proj_w = 0, proj_b = 0;
+  std::vector<float> blob;             // host copy
+  std::vector<int> call_LQ, call_LK, call_U, call_u;
+  std::vector<size_t> idx_off;
+  size_t idx_total = 0;
+  int64_t attn_floats = 0;             // per sequence
+  // device state
+  float* d_blob = nullptr;
+  size_t d_blob_n = 0;
+  float* ws = nullptr;
+  size_t ws_n = 0;
+  int32_t* d_idx = nullptr;
+  ~Model();
+  int upload();
+  // x_enc [B][L0][C], x_dec [B][Ld][C] → out [B][pred][c_out]; idx_dev: this forward's draws (device)
+  int forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
+              hipStream_t st);
+  size_t push(const std::vector<float>& v);
+};
+
+}  // namespace lw
+}  // namespace cet

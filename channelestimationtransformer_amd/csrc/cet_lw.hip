@@ -1,0 +1,348 @@
+// Layer-wise engine for shapes outside the fused kernels (any d_model, n_heads with d_k = d_model //
+// n_heads, d_ff, sequence lengths up to LW_LMAX): one launch per operator, activations fp32 in HBM,
+// every contraction on the fp32-input MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, the
+// reference's own arithmetic class, so the ProbSparse top-u selection matches it).
+//
+// Operators (reference behaviour they restate):
+//   lw_gemm       Linear / Conv1d(k=1) / circular Conv1d(k=3) (TokenEmbedding embed.py:30-49, ConvLayer
+//                 encoder.py:22-28) with bias, folded BatchNorm, positional table, activation and residual
+//   lw_layernorm  nn.LayerNorm over the rows (encoder.py:49-56, decoder.py:33-40), output rows remappable
+//                 (EncoderStack concatenation, encoder.py:95-106)
+//   lw_maxpool    MaxPool1d(3, 2, 1) (encoder.py:20,27)
+//   lw_window     x[:, -L:] of EncoderStack (encoder.py:102-104)
+//   lw_attention  ProbAttention (attn.py:73-175) and FullAttention (attn.py:37-70) per (sequence, head),
+//                 with the AttentionLayer mix re-view (attn.py:205-206) and the optional attns maps
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cet_lw.h"
+
+namespace cet {
+namespace lw {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+// ------------------------------------------------------------------------------------ GEMM
+// C[m][n] = epi(Σ_k A(m, k) · W[n][k]); 64 × 64 output tile per 256-thread workgroup, K in steps of
+// 16 staged through LDS; wave w computes rows 16w..16w+15 × the tile's 64 columns (4 accumulators).
+constexpr int GT = 64, GK = 16;
+
+__device__ __forceinline__ float load_a(const GemmOp& op, int m, int k) {
+  if (m >= op.M || k >= op.K) return 0.f;
+  if (op.amode == 0) return op.A[(size_t)m * op.lda + k];
+  // circular k=3 conv over each sequence: m = b·L + t, k = tap·C + c → src row (t − 1 + tap) mod L
+  const int b = m / op.L, t = m - b * op.L;
+  const int tap = k / op.Cin, c = k - tap * op.Cin;
+  int r = t - 1 + tap;
+  r = r < 0 ? r + op.L : (r >= op.L ? r - op.L : r);
+  return op.A[((size_t)b * op.Ls + op.off + r) * op.lda + c];
+}
+
+__global__ void __launch_bounds__(256) lw_gemm(GemmOp op) {
+  __shared__ float As[GT][GK + 1];
+  __shared__ float Ws[GT][GK + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * GT, n0 = blockIdx.y * GT;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < op.K; k0 += GK) {
+    // 64 × 16 of A and of W: 1024 elements each, 4 per thread
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, r = e >> 4, c = e & 15;
+      As[r][c] = load_a(op, m0 + r, k0 + c);
+      const int n = n0 + r, k = k0 + c;
+      Ws[r][c] = n < op.N && k < op.K ? op.W[(size_t)n * op.K + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GK; kk += 4) {
+      const float a = As[16 * w + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float b = Ws[16 * j + (lane & 15)][kk + (lane >> 4)];
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // epilogue: lane holds rows 4(lane>>4)+r of the wave's 16, column lane&15 of each 16-wide group
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + 16 * j + (lane & 15);
+    if (n >= op.N) continue;
+    const float sc = op.scale ? op.scale[n] : 1.f;
+    const float bi = op.bias ? op.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 16 * w + 4 * (lane >> 4) + r;
+      if (m >= op.M) continue;
+      float y = acc[j][r] * sc + bi;
+      const int b = m / op.L, t = m - b * op.L;
+      if (op.pe) y += op.pe[(size_t)t * op.N + n];
+      if (op.act == 1) y = gelu(y);
+      else if (op.act == 2) y = fmaxf(y, 0.f);
+      else if (op.act == 3) y = y > 0.f ? y : expm1f(y);
+      if (op.R) y += op.R[(size_t)m * op.ldr + n];
+      if (op.row_t0 > 0) {   // keep rows t ≥ t0 of every sequence, written as [b][t − t0]
+        if (t < op.row_t0) continue;
+        op.Y[((size_t)b * (op.L - op.row_t0) + (t - op.row_t0)) * op.ldy + n] = y;
+      } else {
+        op.Y[(size_t)m * op.ldy + n] = y;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- LayerNorm
+// One wave per row; Y[out_row(m)] = (X[m] − mean) / sqrt(var + eps) · g + b  (biased variance).
+__global__ void __launch_bounds__(256) lw_layernorm(LnOp op) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= op.M) return;
+  const float* x = op.X + (size_t)m * op.D;
+  float v[LW_DMAX / 64];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LW_DMAX / 64; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < op.D ? x[c] : 0.f;
+    s += v[i];
+  }
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)op.D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LW_DMAX / 64; ++i) {
+    const int c = lane + 64 * i;
+    const float d = c < op.D ? v[i] - mean : 0.f;
+    q = fmaf(d, d, q);
+  }
+  for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float inv = 1.0f / sqrtf(q / (float)op.D + 1e-5f);
+  const int b = m / op.L, t = m - b * op.L;
+  float* y = op.Y + ((size_t)b * op.Lo + op.off + t) * op.D;
+#pragma unroll
+  for (int i = 0; i < LW_DMAX / 64; ++i) {
+    const int c = lane + 64 * i;
+    if (c < op.D) y[c] = (v[i] - mean) * inv * op.g[c] + op.b[c];
+  }
+}
+
+// ---------------------------------------------------------------------- MaxPool / window copy
+__global__ void lw_maxpool(const float* __restrict__ X, float* __restrict__ Y, int B, int L, int Lo, int D) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * Lo * D) return;
+  const int c = (int)(i % D);
+  const int64_t r = i / D;
+  const int t = (int)(r % Lo), b = (int)(r / Lo);
+  const float* x = X + (size_t)b * L * D + c;
+  float v = x[(size_t)(2 * t) * D];
+  if (2 * t + 1 < L) v = fmaxf(v, x[(size_t)(2 * t + 1) * D]);
+  if (2 * t - 1 >= 0) v = fmaxf(v, x[(size_t)(2 * t - 1) * D]);
+  Y[i] = v;
+}
+
+__global__ void lw_window(const float* __restrict__ X, float* __restrict__ Y, int B, int L0, int L, int D) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * L * D) return;
+  const int c = (int)(i % D);
+  const int64_t r = i / D;
+  const int t = (int)(r % L), b = (int)(r / L);
+  Y[i] = X[((size_t)b * L0 + (L0 - L) + t) * D + c];
+}
+
+// ------------------------------------------------------------------------------- attention
+// One 256-thread workgroup per (sequence, head).  S = Q_h·K_hᵀ for every (query, key) pair in LDS,
+// accumulated over feature chunks of 32 on the f32 MFMA; then per query row: ProbSparse M from the
+// sampled pairs (attn.py:89-105, sum divided by L_K), exact top-u by rank (ties to the lower index),
+// the initial context (mean(V) or cumsum(V) if masked, :116-125), and softmax(scale·S)·V for the
+// selected (or all) rows with the causal mask (:127-146, ProbMask :23-34 / TriangularCausalMask
+// :10-20).  scale = 1/sqrt(d_k) (attn.py:81,163).
+constexpr int AC = 32;   // feature chunk
+__global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int LQ = op.LQ, LK = op.LK, E = op.E;
+  const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15;
+  float* S = sm;                                   // [LQp][LKp + 1]
+  const int SS = LKp + 1;
+  float* Qc = S + LQp * SS;                        // [LQp][AC + 1]
+  float* Kc = Qc + LQp * (AC + 1);                 // [LKp][AC + 1]
+  float* Mv = Kc + LKp * (AC + 1);                 // [LQp] sparsity measure
+  int* sel = reinterpret_cast<int*>(Mv + LQp);     // [LQp] selected query of rank r
+  int* flag = sel + LQp;                           // [LQp] row selected
+  const int b = blockIdx.x / op.H, h = blockIdx.x - (blockIdx.x / op.H) * op.H;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* Qg = op.Q + (size_t)b * LQ * op.ldq + (size_t)h * E;
+  const float* Kg = op.K + (size_t)b * LK * op.ldk + (size_t)h * E;
+  const float* Vg = op.V + (size_t)b * LK * op.ldv + (size_t)h * E;
+  const int nqt = LQp / 16, nkt = LKp / 16;
+
+  // ---- S = Q·Kᵀ, tile (qt, kt) owned by wave (qt·nkt + kt) mod 4, accumulated in LDS across chunks
+  for (int i = tid; i < LQp * SS; i += 256) S[i] = 0.f;
+  for (int e0 = 0; e0 < E; e0 += AC) {
+    __syncthreads();
+    for (int i = tid; i < LQp * AC; i += 256) {
+      const int r = i / AC, c = i - r * AC;
+      Qc[r * (AC + 1) + c] = r < LQ && e0 + c < E ? Qg[(size_t)r * op.ldq + e0 + c] : 0.f;
+    }
+    for (int i = tid; i < LKp * AC; i += 256) {
+      const int r = i / AC, c = i - r * AC;
+      Kc[r * (AC + 1) + c] = r < LK && e0 + c < E ? Kg[(size_t)r * op.ldk + e0 + c] : 0.f;
+    }
+    __syncthreads();
+    for (int t = w; t < nqt * nkt; t += 4) {
+      const int qt = t / nkt, kt = t - qt * nkt;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < AC; kk += 4) {
+        const float a = Qc[(16 * qt + (lane & 15)) * (AC + 1) + kk + (lane >> 4)];
+        const float bb = Kc[(16 * kt + (lane & 15)) * (AC + 1) + kk + (lane >> 4)];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[(16 * qt + 4 * (lane >> 4) + r) * SS + 16 * kt + (lane & 15)] += acc[r];
+    }
+  }
+  __syncthreads();
+
+  const bool sparse = op.prob && op.u < LQ;
+  // ---- ProbSparse: M per query from its sampled keys, then the top-u by rank
+  if (sparse) {
+    for (int q = tid; q < LQ; q += 256) {
+      const int32_t* ix = op.idx + (size_t)q * op.U;
+      float mx = -INFINITY, sum = 0.f;
+      for (int j = 0; j < op.U; ++j) {
+        const float s = S[q * SS + ix[j]];
+        mx = fmaxf(mx, s);
+        sum += s;
+      }
+      Mv[q] = mx - sum / (float)LK;
+    }
+    __syncthreads();
+    for (int q = tid; q < LQ; q += 256) {
+      const float m = Mv[q];
+      int rank = 0;
+      for (int j = 0; j < LQ; ++j) {
+        const float o = Mv[j];
+        rank += (o > m) || (o == m && j < q);
+      }
+      flag[q] = rank < op.u;
+      if (rank < op.u) sel[rank] = q;
+    }
+    __syncthreads();
+  }
+  const int nsel = sparse ? op.u : LQ;
+  const float scale = 1.0f / sqrtf((float)E);
+
+  // output placement: (query i, head h, feature e) → ctx; mix re-views (L, H, E) as (H, L, E)
+  auto ctx_ptr = [&](int i) -> float* {
+    if (!op.mix) return op.O + ((size_t)b * LQ + i) * op.ldo + (size_t)h * E;
+    return op.O + (size_t)b * LQ * op.ldo + (size_t)h * LQ * E + (size_t)i * E;
+  };
+
+  // ---- unselected rows: the initial context
+  if (sparse) {
+    for (int e = tid; e < E; e += 256) {
+      if (!op.causal) {
+        float s = 0.f;
+        for (int j = 0; j < LK; ++j) s += Vg[(size_t)j * op.ldv + e];
+        const float mean = s / (float)LK;
+        for (int q = 0; q < LQ; ++q)
+          if (!flag[q]) ctx_ptr(q)[e] = mean;
+      } else {
+        float s = 0.f;
+        for (int q = 0; q < LQ; ++q) {
+          s += Vg[(size_t)q * op.ldv + e];
+          if (!flag[q]) ctx_ptr(q)[e] = s;
+        }
+      }
+    }
+    if (op.attns) {
+      float* A = op.attns + (size_t)b * op.attn_bstride + (size_t)h * LQ * LK;
+      for (int i = tid; i < LQ * LK; i += 256)
+        if (!flag[i / LK]) A[i] = 1.0f / (float)LK;
+    }
+  }
+
+  // ---- softmax rows of the selected queries (P written over S in place), one wave per row
+  for (int r = w; r < nsel; r += 4) {
+    const int q = sparse ? sel[r] : r;
+    float* Srow = S + q * SS;
+    const int kmax = op.causal ? q + 1 : LK;   // keys j > q masked
+    float mx = -INFINITY;
+    for (int j = lane; j < kmax; j += 64) mx = fmaxf(mx, Srow[j] * scale);
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float sum = 0.f;
+    for (int j = lane; j < LK; j += 64) {
+      const float p = j < kmax ? expf(Srow[j] * scale - mx) : 0.f;
+      Srow[j] = p;
+      sum += p;
+    }
+    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    const float inv = 1.0f / sum;
+    for (int j = lane; j < LK; j += 64) Srow[j] *= inv;
+    if (op.attns) {
+      float* A = op.attns + (size_t)b * op.attn_bstride + ((size_t)h * LQ + q) * LK;
+      for (int j = lane; j < LK; j += 64) A[j] = Srow[j];
+    }
+  }
+  __syncthreads();
+  // ---- O = P·V for the selected rows: thread per (row, feature), V read from global (L2)
+  for (int i = tid; i < nsel * E; i += 256) {
+    const int r = i / E, e = i - r * E;
+    const int q = sparse ? sel[r] : r;
+    const float* Prow = S + q * SS;
+    float o = 0.f;
+    for (int j = 0; j < LK; ++j) o = fmaf(Prow[j], Vg[(size_t)j * op.ldv + e], o);
+    ctx_ptr(q)[e] = o;
+  }
+}
+
+size_t attn_lds_bytes(int LQ, int LK) {
+  const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15;
+  return sizeof(float) * ((size_t)LQp * (LKp + 1) + (size_t)LQp * (AC + 1) + (size_t)LKp * (AC + 1) + LQp) +
+         sizeof(int) * 2 * (size_t)LQp;
+}
+
+// ---------------------------------------------------------------------------------- launchers
+int launch_gemm(const GemmOp& op, hipStream_t st) {
+  if (op.M <= 0 || op.N <= 0) return 0;
+  dim3 grid((op.M + GT - 1) / GT, (op.N + GT - 1) / GT);
+  hipLaunchKernelGGL(lw_gemm, grid, dim3(256), 0, st, op);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int launch_layernorm(const LnOp& op, hipStream_t st) {
+  if (op.D > LW_DMAX) return -3;
+  hipLaunchKernelGGL(lw_layernorm, dim3((op.M + 3) / 4), dim3(256), 0, st, op);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int launch_maxpool(const float* X, float* Y, int B, int L, int Lo, int D, hipStream_t st) {
+  const int64_t n = (int64_t)B * Lo * D;
+  hipLaunchKernelGGL(lw_maxpool, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, Y, B, L, Lo, D);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStream_t st) {
+  const int64_t n = (int64_t)B * L * D;
+  hipLaunchKernelGGL(lw_window, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, Y, B, L0, L, D);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int launch_attention(const AttnOp& op, int B, hipStream_t st) {
+  if (op.LQ > LW_LMAX || op.LK > LW_LMAX) return -3;
+  const size_t lds = attn_lds_bytes(op.LQ, op.LK);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(lw_attention), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return -1;
+    attr = true;
+  }
+  hipLaunchKernelGGL(lw_attention, dim3(B * op.H), dim3(256), lds, st, op);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace lw
+}  // namespace cet

@@ -1,0 +1,177 @@
+// Layer-wise engine, host side: the forward of InformerStack / Informer (FullPrecision/InformerModel/
+// model.py:11-271) as a sequence of operator launches on the caller's stream (cet_lw.hip), for the
+// shapes the fused kernels do not carry.  The model (weights as fp32 [N][K] matrices, the plan of
+// layers) is built by cet_api.cpp (build_lw); this file owns the device side.
+#include <algorithm>
+
+#include "cet_lw.h"
+
+namespace cet {
+namespace lw {
+
+Model::~Model() {
+  if (d_blob) (void)hipFree(d_blob);
+  if (ws) (void)hipFree(ws);
+  if (d_idx) (void)hipFree(d_idx);
+}
+
+size_t Model::push(const std::vector<float>& v) {
+  while (blob.size() % 4) blob.push_back(0.f);
+  const size_t off = blob.size();
+  blob.insert(blob.end(), v.begin(), v.end());
+  return off;
+}
+
+int Model::upload() {
+  if (blob.size() > d_blob_n) {
+    if (d_blob && hipFree(d_blob) != hipSuccess) return -1;
+    d_blob = nullptr;
+    if (hipMalloc((void**)&d_blob, blob.size() * sizeof(float)) != hipSuccess) return -1;
+    d_blob_n = blob.size();
+  }
+  if (hipMemcpy(d_blob, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (!d_idx && idx_total && hipMalloc((void**)&d_idx, idx_total * sizeof(int32_t)) != hipSuccess) return -1;
+  return 0;
+}
+
+int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
+                   hipStream_t st) {
+  const int Lm = std::max(L0, Ld);
+  const size_t BL0 = (size_t)B * L0, BLm = (size_t)B * std::max(Lm, S);
+  // workspace: E0 | X | QKV | CTX | HID | ENC | XD | QC
+  const size_t nE0 = BL0 * D, nX = BL0 * D, nQKV = BLm * 3 * HE, nCTX = BLm * HE,
+               nHID = BLm * std::max(dff, D), nENC = (size_t)B * S * D, nXD = (size_t)B * Ld * D,
+               nQC = (size_t)B * Ld * HE;
+  const size_t need = nE0 + nX + nQKV + nCTX + nHID + nENC + nXD + nQC + 64;
+  if (need > ws_n) {
+    if (ws && hipFree(ws) != hipSuccess) return -1;
+    ws = nullptr;
+    if (hipMalloc((void**)&ws, need * sizeof(float)) != hipSuccess) return -1;
+    ws_n = need;
+  }
+  float* E0 = ws;
+  float* X = E0 + nE0;
+  float* QKV = X + nX;
+  float* CTX = QKV + nQKV;
+  float* HID = CTX + nCTX;
+  float* ENC = HID + nHID;
+  float* XD = ENC + nENC;
+  float* QC = XD + nXD;
+  const float* P = d_blob;
+  int rc = 0;
+  auto gemm = [&](const float* A, int M, int N, int K, int lda, size_t w, size_t bias, float* Y, int ldy,
+                  int Lrow) {
+    GemmOp g{};
+    g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.amode = 0; g.L = Lrow; g.Ls = Lrow; g.off = 0; g.Cin = 1;
+    g.W = P + w; g.bias = P + bias; g.scale = nullptr; g.pe = nullptr; g.act = 0; g.R = nullptr; g.ldr = 0;
+    g.Y = Y; g.ldy = ldy; g.row_t0 = 0;
+    return g;
+  };
+  auto run = [&](const GemmOp& g) {
+    if (!rc) rc = launch_gemm(g, st);
+  };
+  auto ln = [&](float* Xi, float* Yo, int M, int L, int Lo, int off, size_t g, size_t b) {
+    LnOp o{M, D, L, Lo, off, Xi, Yo, P + g, P + b};
+    if (!rc) rc = launch_layernorm(o, st);
+  };
+  auto attend = [&](const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv, float* O, int LQ,
+                    int LK, int prob_, int causal, int mix_, int call, float* amap) {
+    AttnOp a{};
+    a.H = H; a.E = E; a.LQ = LQ; a.LK = LK; a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.V = V; a.ldv = ldv;
+    a.O = O; a.ldo = HE; a.prob = prob_; a.causal = causal; a.mix = mix_;
+    a.U = call >= 0 ? call_U[call] : 0;
+    a.u = call >= 0 ? call_u[call] : LQ;
+    a.idx = call >= 0 ? idx_dev + idx_off[call] : nullptr;
+    a.attns = amap;
+    a.attn_bstride = attn_floats;
+    if (!rc) rc = launch_attention(a, B, st);
+  };
+
+  // ---- DataEmbedding (embed.py:132-135): circular conv k=3 + pe[:L]
+  {
+    GemmOp g = gemm(x_enc, B * L0, D, 3 * C, C, emb_enc_w, emb_enc_b, stack ? E0 : X, D, L0);
+    g.amode = 1; g.Cin = C; g.pe = P + pe_enc;
+    run(g);
+  }
+  // ---- encoders (EncoderStack: encoder i on x[:, -L0/2^i:], encoder.py:95-106)
+  for (size_t i = 0; i < enc.size(); ++i) {
+    int L = enc_L0[i];
+    if (stack && !rc) rc = launch_window(E0, X, B, L0, L, D, st);
+    for (const EncLayer& ly : enc[i]) {
+      const int M = B * L;
+      run(gemm(X, M, 3 * HE, D, D, ly.wqkv, ly.bqkv, QKV, 3 * HE, L));
+      attend(QKV, 3 * HE, QKV + HE, 3 * HE, QKV + 2 * HE, 3 * HE, CTX, L, L, prob, 0, 0, ly.call,
+             attns && out_attn ? attns + ly.attn_off : nullptr);
+      {
+        GemmOp g = gemm(CTX, M, D, HE, HE, ly.wo, ly.bo, X, D, L);   // x + new_x (encoder.py:49)
+        g.R = X; g.ldr = D;
+        run(g);
+      }
+      ln(X, X, M, L, L, 0, ly.g1, ly.be1);
+      {
+        GemmOp g = gemm(X, M, dff, D, D, ly.w1, ly.b1, HID, dff, L);
+        g.act = act;
+        run(g);
+        GemmOp g2 = gemm(HID, M, D, dff, dff, ly.w2, ly.b2, X, D, L);
+        g2.R = X; g2.ldr = D;
+        run(g2);
+      }
+      ln(X, X, M, L, L, 0, ly.g2, ly.be2);
+      if (ly.conv) {   // ConvLayer (encoder.py:22-28)
+        GemmOp g = gemm(X, M, D, 3 * D, D, ly.wc, ly.sh, HID, D, L);
+        g.amode = 1; g.Cin = D; g.scale = P + ly.sc; g.act = 3;
+        run(g);
+        if (!rc) rc = launch_maxpool(HID, X, B, L, ly.L_out, D, st);
+        L = ly.L_out;
+      }
+    }
+    // Encoder.norm → rows [enc_off, enc_off + L) of the concatenated stack output
+    ln(X, ENC, B * L, L, S, enc_off[i], norm_g[i], norm_b[i]);
+  }
+  // ---- decoder (decoder.py:43-56, model.py:211-225)
+  {
+    GemmOp g = gemm(x_dec, B * Ld, D, 3 * Cd, Cd, emb_dec_w, emb_dec_b, XD, D, Ld);
+    g.amode = 1; g.Cin = Cd; g.pe = P + pe_dec;
+    run(g);
+  }
+  const int Md = B * Ld;
+  for (const DecLayer& ly : dec) {
+    run(gemm(XD, Md, 3 * HE, D, D, ly.wqkv, ly.bqkv, QKV, 3 * HE, Ld));
+    attend(QKV, 3 * HE, QKV + HE, 3 * HE, QKV + 2 * HE, 3 * HE, CTX, Ld, Ld, prob, 1, mix, ly.call, nullptr);
+    {
+      GemmOp g = gemm(CTX, Md, D, HE, HE, ly.wo, ly.bo, XD, D, Ld);
+      g.R = XD; g.ldr = D;
+      run(g);
+    }
+    ln(XD, XD, Md, Ld, Ld, 0, ly.g1, ly.be1);
+    run(gemm(XD, Md, HE, D, D, ly.wcq, ly.bcq, QC, HE, Ld));
+    run(gemm(ENC, B * S, 2 * HE, D, D, ly.wckv, ly.bckv, QKV, 2 * HE, S));
+    attend(QC, HE, QKV, 2 * HE, QKV + HE, 2 * HE, CTX, Ld, S, 0, 0, 0, -1, nullptr);
+    {
+      GemmOp g = gemm(CTX, Md, D, HE, HE, ly.wco, ly.bco, XD, D, Ld);
+      g.R = XD; g.ldr = D;
+      run(g);
+    }
+    ln(XD, XD, Md, Ld, Ld, 0, ly.g2, ly.be2);
+    {
+      GemmOp g = gemm(XD, Md, dff, D, D, ly.w1, ly.b1, HID, dff, Ld);
+      g.act = act;
+      run(g);
+      GemmOp g2 = gemm(HID, Md, D, dff, dff, ly.w2, ly.b2, XD, D, Ld);
+      g2.R = XD; g2.ldr = D;
+      run(g2);
+    }
+    ln(XD, XD, Md, Ld, Ld, 0, ly.g3, ly.be3);
+  }
+  ln(XD, XD, Md, Ld, Ld, 0, dnorm_g, dnorm_b);
+  {
+    // projection (model.py:264), the last pred_len rows of every sequence → out[B][pred][c_out]
+    GemmOp g = gemm(XD, Md, c_out, D, D, proj_w, proj_b, out, c_out, Ld);
+    g.row_t0 = Ld - pred;   // (0: every row kept, the plain row map)
+    run(g);
+  }
+  return rc;
+}
+
+}  // namespace lw
+}  // namespace cet

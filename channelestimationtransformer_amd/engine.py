@@ -155,10 +155,11 @@ class Engine:
         """Fused-kernel generation: 4 (default), 3 (bf16-only predecessor) or 1 (LDS-resident)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
 
-    PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2}
+    PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3}
 
     def set_precision(self, prec) -> None:
-        """Dense-layer operand precision of the v4 kernel: "auto", "bf16", "split-bf16" or "fp8" (include/cet.h)."""
+        """Dense-layer operand precision of the v4 kernel: "auto", "bf16", "split-bf16" or "fp8" (include/cet.h).
+        Engines on the layer-wise path (shapes outside the fused kernels) report "fp32-layerwise"."""
         code = self.PRECISIONS[prec] if isinstance(prec, str) else int(prec)
         check(lib.cet_set_precision(self._h, code), "cet_set_precision")
 

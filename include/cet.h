@@ -128,7 +128,11 @@ int cet_set_variant(cet_engine* e, int variant);
  *    0 bf16 operands, fp32 accumulation / LayerNorm / softmax (the C2 contract);
  *    1 split bf16 (hi + lo per operand, three MFMAs per product): fp32-level parity;
  *    2 fp8 (OCP e4m3) activations on the fp8 MFMA for the LSQ-quantised layers, the integer weight
- *      grid carried exactly as two e4m3 parts (LSQ engines of at most 8 bits).
+ *      grid carried exactly as two e4m3 parts (LSQ engines of at most 8 bits);
+ *    3 (reported only) the layer-wise engine: models the fused kernels cannot carry (d_model != 128,
+ *      n_heads != 8, d_ff > 128, more than 96 encoder / 48 decoder rows; up to d_model 1024 and 128
+ *      rows) run as one launch per operator with fp32 operands on the f32 MFMA (cet_lw.hip).
+ *      CET_LAYERWISE=1 in the environment at cet_create_informer routes any model there.
  * cet_get_precision() returns the precision the packed plan uses (packs the weights if needed).
  * Replaces nothing in the reference, which computes in fp32 (FullPrecision/InformerModel) or with
  * fp32 fake-quantised weights (models/InformerLSQ/LSQ.py:65-74). */

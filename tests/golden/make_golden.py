@@ -60,6 +60,19 @@ CASES = {
     "informer_lsq11": dict(model="informer_lsq", cfg=dict(num_bits=11), B=2, acts=False),
     # single-encoder Informer (FullPrecision/InformerModel/model.py:11-139), e_layers an int
     "informer_single_e3": dict(model="informer", cfg=dict(e_layers=3), B=2, acts=True),
+    # shapes outside the fused kernels (the layer-wise engine): the MimoSimulation checkpoint's
+    # d_model 64 with e_layers [4,3]; the TimingAnalysis sweeps' n_heads that do not divide d_model
+    # (d_keys = d_model // n_heads, TrainInformer.py:236-264), d_ff and d_model beyond 128, and a
+    # long, genuinely sparse decoder (label_len 25 + pred_len 9)
+    "informer_d64_e43": dict(model="informer_stack", cfg=dict(d_model=64, e_layers=[4, 3]), B=2, acts=True),
+    "informer_h5_ff256": dict(model="informer_stack", cfg=dict(n_heads=5, d_ff=256), B=2, acts=False),
+    "informer_d256_h3_lab25": dict(model="informer_stack",
+                                   cfg=dict(d_model=256, n_heads=3, d_ff=128, seq_len=48, label_len=25, pred_len=9),
+                                   B=2, acts=False),
+    "informer_full_d512_h4": dict(model="informer_stack",
+                                  cfg=dict(attn="full", d_model=512, n_heads=4, d_ff=512, e_layers=[2], d_layers=1,
+                                           seq_len=24, label_len=8, pred_len=3),
+                                  B=2, acts=True),
 }
 
 

@@ -38,6 +38,12 @@ def case_names():
     return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("data_"))
 
 
+def layerwise_name(name: str) -> bool:
+    """Fixture cases whose shapes only the layer-wise engine carries (d_model != 128, n_heads != 8,
+    d_ff > 128, more than 48 decoder rows); their names say so."""
+    return any(t in name for t in ("_d64_", "_h5_", "_d256_", "_d512_"))
+
+
 def load_case(name: str) -> Case:
     with np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False) as f:
         z = {k: f[k] for k in f.files}

@@ -80,9 +80,35 @@ def test_unsupported_config_fails_loudly():
     from channelestimationtransformer_amd.engine import Engine
     from channelestimationtransformer_amd.informer import InformerStack
 
-    m = InformerStack(16, 16, 16, 90, 10, 5, 5, 64, 8, [4], 3, 64)
+    m = InformerStack(16, 16, 16, 90, 10, 5, 5, 2048, 8, [4], 3, 64)
     with pytest.raises(CetError, match="d_model"):
         Engine.informer(m.config())
+    m = InformerStack(16, 16, 16, 200, 10, 5, 5, 128, 8, [4], 3, 64)
+    with pytest.raises(CetError, match="seq_len"):
+        Engine.informer(m.config())
+
+
+def test_layerwise_engine_plans_on_the_host():
+    """Shapes outside the fused kernels (the MimoSimulation checkpoint's d_model 64, the TimingAnalysis
+    sweep's 5 heads of 25 with d_ff 256) build the layer-wise plan: weights by reference key name
+    (q/k/v projections d_model → (d_model // n_heads)·n_heads), attention-map layout H·L·L per
+    encoder layer.  Host only (no GPU)."""
+    from channelestimationtransformer_amd.engine import Engine
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+
+    for d_model, heads, dff, e_layers in ((64, 8, 64, [4, 3]), (128, 5, 256, [4])):
+        m = InformerStack(16, 16, 16, 90, 10, 5, 5, d_model, heads, e_layers, 3, dff, 0.05, "prob", "fixed",
+                          "gelu", True, True)
+        eng = Engine.informer(m.config())
+        state = synthetic_state_dict(m._schema(), 0)
+        assert state["encoder.encoders.0.attn_layers.0.attention.query_projection.weight"].shape == \
+            ((d_model // heads) * heads, d_model)
+        eng.load_state_dict(state)
+        lay = eng.attns_layout()
+        assert [L for _, L in lay][:4] == [90, 45, 23, 12]
+        assert eng.attns_floats() == sum(heads * L * L for _, L in lay)
+        assert eng.precision() == "fp32-layerwise"
 
 
 def test_forward_refuses_cpu_tensors():

@@ -8,12 +8,13 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import case_names, load_case, rel_nmse
+from golden_util import case_names, layerwise_name, load_case, rel_nmse
 
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
-INFORMER_CASES = [n for n in case_names() if n.startswith("informer")]
+# the fused kernels' cases (the layer-wise engine's shapes: tests/test_gpu_layerwise.py)
+INFORMER_CASES = [n for n in case_names() if n.startswith("informer") and not layerwise_name(n)]
 
 
 def _gpu():
