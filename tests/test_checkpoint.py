@@ -43,3 +43,30 @@ def test_json_export_roundtrip(tmp_path):
     assert set(back) == set(case.state)
     for k, v in case.state.items():
         np.testing.assert_array_equal(back[k], v)
+
+
+def test_trained_mimo_checkpoint_drops_into_the_engine():
+    """The only trained weights in the reference (MimoSimulation/models/checkpoint/checkpoint.pth,
+    loaded by MimoSimulation/Predict.py:91-93 for InformerStack(16,16,16, 25,10,5, 5, d_model 64, 8,
+    e_layers [4,3], 3, 64, attn "full")): read with torch.load(weights_only=True), loaded with the
+    callers' strict=False, and planned by the layer-wise engine (d_model 64 is outside the fused
+    kernels).  Host only; skipped where the reference tree is absent (it never travels)."""
+    import os
+
+    import pytest
+
+    path = "/root/reference/MimoSimulation/models/checkpoint/checkpoint.pth"
+    if not os.path.exists(path):
+        pytest.skip("reference tree absent")
+    from channelestimationtransformer_amd.engine import Engine
+
+    sd = torch.load(path, weights_only=True, map_location="cpu")["state_dict"]
+    m = InformerStack(16, 16, 16, 25, 10, 5, 5, 64, 8, [4, 3], 3, 64, 0.05, "full", "fixed", "gelu", True, True,
+                      torch.device("cpu"))
+    res = m.load_state_dict(sd, strict=False)
+    assert not res.unexpected_keys
+    assert all(".temporal_embedding." in k for k in res.missing_keys)   # unused tables (embed.py:132-135)
+    eng = Engine.informer(m.config())
+    eng.load_state_dict({k: v.numpy() for k, v in m.state_dict().items()})
+    assert eng.precision() == "fp32-layerwise"
+    assert [L for _, L in eng.attns_layout()] == [25, 13, 7, 4, 12, 6, 3]
