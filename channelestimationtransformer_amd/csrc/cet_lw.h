@@ -67,6 +67,7 @@ int launch_maxpool(const float* X, float* Y, int B, int L, int Lo, int D, hipStr
 int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStream_t st);
 int launch_attention(const AttnOp& op, int B, hipStream_t st);
 size_t attn_lds_bytes(int LQ, int LK);
+int prepare_attention();   // dynamic-LDS attribute of lw_attention (before any capture)
 
 // ------------------------------------------------------------------ host model (cet_lw_host.cpp)
 // Weights as fp32 [N][K] matrices in one device blob (float offsets below); ProbSparse draws of a
@@ -102,7 +103,14 @@ struct Model {
   float* ws = nullptr;
   size_t ws_n = 0;
   int32_t* d_idx = nullptr;
+  hipGraphExec_t gexec = nullptr;   // the operator sequence captured for batch gB
+  int gB = 0;
+  hipStream_t cap = nullptr;        // capture stream
   ~Model();
+  size_t ws_floats(int B) const;
+  int ensure_ws(int B);
+  int enqueue(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
+              hipStream_t st);
   int upload();
   // x_enc [B][L0][C], x_dec [B][Ld][C] → out [B][pred][c_out]; idx_dev: this forward's draws (device)
   int forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,

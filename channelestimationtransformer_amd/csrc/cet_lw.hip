@@ -97,6 +97,78 @@ __global__ void __launch_bounds__(256) lw_gemm(GemmOp op) {
   }
 }
 
+// Short-M variant (batch-1 latency: M = a few sequences' rows): a 16 × 64 tile per workgroup, so the
+// ≈100-row GEMMs of one sequence spread over 6× more workgroups; K staged in chunks of 64 with the
+// next chunk's global loads in flight during this chunk's MFMAs; two accumulation chains per wave.
+constexpr int SM = 16, SK = 64;
+__global__ void __launch_bounds__(256) lw_gemm_s(GemmOp op) {
+  __shared__ float As[SM][SK + 1];
+  __shared__ float Ws[GT][SK + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * SM, n0 = blockIdx.y * GT;
+  float ra[SM * SK / 256], rw[GT * SK / 256];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < SM * SK / 256; ++i) {
+      const int e = tid + 256 * i, r = e / SK, c = e % SK;
+      ra[i] = load_a(op, m0 + r, k0 + c);
+    }
+#pragma unroll
+    for (int i = 0; i < GT * SK / 256; ++i) {
+      const int e = tid + 256 * i, r = e / SK, c = e % SK;
+      const int n = n0 + r, k = k0 + c;
+      rw[i] = n < op.N && k < op.K ? op.W[(size_t)n * op.K + k] : 0.f;
+    }
+  };
+  fetch(0);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  for (int k0 = 0; k0 < op.K; k0 += SK) {
+    __syncthreads();   // the previous chunk has been read
+#pragma unroll
+    for (int i = 0; i < SM * SK / 256; ++i) {
+      const int e = tid + 256 * i;
+      As[e / SK][e % SK] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < GT * SK / 256; ++i) {
+      const int e = tid + 256 * i;
+      Ws[e / SK][e % SK] = rw[i];
+    }
+    __syncthreads();
+    if (k0 + SK < op.K) fetch(k0 + SK);
+#pragma unroll
+    for (int kk = 0; kk < SK; kk += 8) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(As[lane & 15][kk + (lane >> 4)],
+                                                  Ws[16 * w + (lane & 15)][kk + (lane >> 4)], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(As[lane & 15][kk + 4 + (lane >> 4)],
+                                                  Ws[16 * w + (lane & 15)][kk + 4 + (lane >> 4)], acc1, 0, 0, 0);
+    }
+  }
+  const f32x4 acc = acc0 + acc1;
+  const int n = n0 + 16 * w + (lane & 15);
+  if (n >= op.N) return;
+  const float sc = op.scale ? op.scale[n] : 1.f;
+  const float bi = op.bias ? op.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + 4 * (lane >> 4) + r;
+    if (m >= op.M) continue;
+    float y = acc[r] * sc + bi;
+    const int b = m / op.L, t = m - b * op.L;
+    if (op.pe) y += op.pe[(size_t)t * op.N + n];
+    if (op.act == 1) y = gelu(y);
+    else if (op.act == 2) y = fmaxf(y, 0.f);
+    else if (op.act == 3) y = y > 0.f ? y : expm1f(y);
+    if (op.R) y += op.R[(size_t)m * op.ldr + n];
+    if (op.row_t0 > 0) {
+      if (t < op.row_t0) continue;
+      op.Y[((size_t)b * (op.L - op.row_t0) + (t - op.row_t0)) * op.ldy + n] = y;
+    } else {
+      op.Y[(size_t)m * op.ldy + n] = y;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------- LayerNorm
 // One wave per row; Y[out_row(m)] = (X[m] − mean) / sqrt(var + eps) · g + b  (biased variance).
 __global__ void __launch_bounds__(256) lw_layernorm(LnOp op) {
@@ -244,30 +316,6 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
     return op.O + (size_t)b * LQ * op.ldo + (size_t)h * LQ * E + (size_t)i * E;
   };
 
-  // ---- unselected rows: the initial context
-  if (sparse) {
-    for (int e = tid; e < E; e += 256) {
-      if (!op.causal) {
-        float s = 0.f;
-        for (int j = 0; j < LK; ++j) s += Vg[(size_t)j * op.ldv + e];
-        const float mean = s / (float)LK;
-        for (int q = 0; q < LQ; ++q)
-          if (!flag[q]) ctx_ptr(q)[e] = mean;
-      } else {
-        float s = 0.f;
-        for (int q = 0; q < LQ; ++q) {
-          s += Vg[(size_t)q * op.ldv + e];
-          if (!flag[q]) ctx_ptr(q)[e] = s;
-        }
-      }
-    }
-    if (op.attns) {
-      float* A = op.attns + (size_t)b * op.attn_bstride + (size_t)h * LQ * LK;
-      for (int i = tid; i < LQ * LK; i += 256)
-        if (!flag[i / LK]) A[i] = 1.0f / (float)LK;
-    }
-  }
-
   // ---- softmax rows of the selected queries (P written over S in place), one wave per row
   for (int r = w; r < nsel; r += 4) {
     const int q = sparse ? sel[r] : r;
@@ -290,15 +338,54 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
       for (int j = lane; j < LK; j += 64) A[j] = Srow[j];
     }
   }
-  __syncthreads();
-  // ---- O = P·V for the selected rows: thread per (row, feature), V read from global (L2)
-  for (int i = tid; i < nsel * E; i += 256) {
-    const int r = i / E, e = i - r * E;
-    const int q = sparse ? sel[r] : r;
-    const float* Prow = S + q * SS;
-    float o = 0.f;
-    for (int j = 0; j < LK; ++j) o = fmaf(Prow[j], Vg[(size_t)j * op.ldv + e], o);
-    ctx_ptr(q)[e] = o;
+  if (sparse && op.attns) {
+    float* A = op.attns + (size_t)b * op.attn_bstride + (size_t)h * LQ * LK;
+    for (int i = tid; i < LQ * LK; i += 256)
+      if (!flag[i / LK]) A[i] = 1.0f / (float)LK;
+  }
+  // ---- per 32-feature chunk of V (staged in LDS): the initial context of the unselected rows, and
+  //      O = P·V for the selected rows on the f32 MFMA (16 selected rows × 16 features per tile)
+  const int nrt = (nsel + 15) / 16;
+  for (int e0 = 0; e0 < E; e0 += AC) {
+    __syncthreads();   // P complete (first chunk) / the previous chunk's V no longer read
+    for (int i = tid; i < LKp * AC; i += 256) {
+      const int r = i / AC, c = i - r * AC;
+      Kc[r * (AC + 1) + c] = r < LK && e0 + c < E ? Vg[(size_t)r * op.ldv + e0 + c] : 0.f;
+    }
+    __syncthreads();
+    if (sparse && tid < AC && e0 + tid < E) {
+      const int c = tid, e = e0 + tid;
+      if (!op.causal) {   // mean over keys (attn.py:116-119)
+        float sv = 0.f;
+        for (int j = 0; j < LK; ++j) sv += Kc[j * (AC + 1) + c];
+        const float mean = sv / (float)LK;
+        for (int q = 0; q < LQ; ++q)
+          if (!flag[q]) ctx_ptr(q)[e] = mean;
+      } else {            // cumsum over keys (attn.py:120-125)
+        float sv = 0.f;
+        for (int q = 0; q < LQ; ++q) {
+          sv += Kc[q * (AC + 1) + c];
+          if (!flag[q]) ctx_ptr(q)[e] = sv;
+        }
+      }
+    }
+    for (int t = w; t < nrt * (AC / 16); t += 4) {
+      const int rt = t / (AC / 16), et = t - rt * (AC / 16);
+      const int rs = 16 * rt + (lane & 15);
+      const int qa = sparse ? sel[rs < nsel ? rs : nsel - 1] : (rs < nsel ? rs : nsel - 1);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < LKp; k0 += 4) {
+        const float a = S[qa * SS + k0 + (lane >> 4)];
+        const float bb = Kc[(k0 + (lane >> 4)) * (AC + 1) + 16 * et + (lane & 15)];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+      }
+      const int e = e0 + 16 * et + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 16 * rt + 4 * (lane >> 4) + r;
+        if (rr < nsel && e < E) ctx_ptr(sparse ? sel[rr] : rr)[e] = acc[r];
+      }
+    }
   }
 }
 
@@ -311,8 +398,11 @@ size_t attn_lds_bytes(int LQ, int LK) {
 // ---------------------------------------------------------------------------------- launchers
 int launch_gemm(const GemmOp& op, hipStream_t st) {
   if (op.M <= 0 || op.N <= 0) return 0;
-  dim3 grid((op.M + GT - 1) / GT, (op.N + GT - 1) / GT);
-  hipLaunchKernelGGL(lw_gemm, grid, dim3(256), 0, st, op);
+  if (op.M <= 1024) {   // few rows (batch-1 latency): more, shorter workgroups
+    hipLaunchKernelGGL(lw_gemm_s, dim3((op.M + SM - 1) / SM, (op.N + GT - 1) / GT), dim3(256), 0, st, op);
+  } else {
+    hipLaunchKernelGGL(lw_gemm, dim3((op.M + GT - 1) / GT, (op.N + GT - 1) / GT), dim3(256), 0, st, op);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 int launch_layernorm(const LnOp& op, hipStream_t st) {
@@ -330,9 +420,7 @@ int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStre
   hipLaunchKernelGGL(lw_window, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, Y, B, L0, L, D);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
-int launch_attention(const AttnOp& op, int B, hipStream_t st) {
-  if (op.LQ > LW_LMAX || op.LK > LW_LMAX) return -3;
-  const size_t lds = attn_lds_bytes(op.LQ, op.LK);
+int prepare_attention() {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(lw_attention), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -340,7 +428,12 @@ int launch_attention(const AttnOp& op, int B, hipStream_t st) {
       return -1;
     attr = true;
   }
-  hipLaunchKernelGGL(lw_attention, dim3(B * op.H), dim3(256), lds, st, op);
+  return 0;
+}
+int launch_attention(const AttnOp& op, int B, hipStream_t st) {
+  if (op.LQ > LW_LMAX || op.LK > LW_LMAX) return -3;
+  if (prepare_attention()) return -1;
+  hipLaunchKernelGGL(lw_attention, dim3(B * op.H), dim3(256), attn_lds_bytes(op.LQ, op.LK), st, op);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

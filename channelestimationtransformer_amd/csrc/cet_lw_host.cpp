@@ -10,6 +10,8 @@ namespace cet {
 namespace lw {
 
 Model::~Model() {
+  if (gexec) (void)hipGraphExecDestroy(gexec);
+  if (cap) (void)hipStreamDestroy(cap);
   if (d_blob) (void)hipFree(d_blob);
   if (ws) (void)hipFree(ws);
   if (d_idx) (void)hipFree(d_idx);
@@ -31,24 +33,73 @@ int Model::upload() {
   }
   if (hipMemcpy(d_blob, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (!d_idx && idx_total && hipMalloc((void**)&d_idx, idx_total * sizeof(int32_t)) != hipSuccess) return -1;
+  if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) return -1;
+  return prepare_attention() ? -1 : 0;
+}
+
+size_t Model::ws_floats(int B) const {
+  const int Lm = std::max(L0, Ld);
+  const size_t BL0 = (size_t)B * L0, BLm = (size_t)B * std::max(Lm, S);
+  return BL0 * D * 2 + BLm * 3 * HE + BLm * HE + BLm * std::max(dff, D) + (size_t)B * S * D + (size_t)B * Ld * D +
+         (size_t)B * Ld * HE + BL0 * C + (size_t)B * Ld * Cd + (size_t)B * pred * c_out + 64;
+}
+
+int Model::ensure_ws(int B) {
+  const size_t need = ws_floats(B);
+  if (need <= ws_n) return 0;
+  if (gexec) {
+    (void)hipGraphExecDestroy(gexec);
+    gexec = nullptr;
+  }
+  if (ws && hipFree(ws) != hipSuccess) return -1;
+  ws = nullptr;
+  if (hipMalloc((void**)&ws, need * sizeof(float)) != hipSuccess) return -1;
+  ws_n = need;
   return 0;
 }
 
+// The operator sequence is captured once per batch size into a hipGraph over fixed workspace
+// buffers; a forward then costs two input copies, one graph launch and one output copy on the
+// caller's stream instead of ≈110 kernel launches (batch-1 latency is launch-bound).  Forwards that
+// materialise attention maps launch the operators directly.
 int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
+                   hipStream_t st) {
+  if (ensure_ws(B)) return -1;
+  if (attns && out_attn) return enqueue(x_enc, x_dec, B, out, attns, idx_dev, st);
+  const size_t nXE = (size_t)B * L0 * C, nXDi = (size_t)B * Ld * Cd, nOUT = (size_t)B * pred * c_out;
+  float* XE = ws + ws_floats(B) - 64 - nOUT - nXDi - nXE;
+  float* XDi = XE + nXE;
+  float* OUTb = XDi + nXDi;
+  if (hipMemcpyAsync(XE, x_enc, nXE * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess) return -1;
+  if (hipMemcpyAsync(XDi, x_dec, nXDi * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess) return -1;
+  if (!gexec || gB != B) {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    gexec = nullptr;
+    hipGraph_t g = nullptr;
+    // captured on a private stream (the caller's may be the null stream, which cannot capture); the
+    // instantiated graph is launched on the caller's stream
+    if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -1;
+    const int rc = enqueue(XE, XDi, B, OUTb, nullptr, idx_dev, cap);
+    if (hipStreamEndCapture(cap, &g) != hipSuccess || rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return -1;
+    }
+    const hipError_t ie = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) return -1;
+    gB = B;
+  }
+  if (hipGraphLaunch(gexec, st) != hipSuccess) return -1;
+  return hipMemcpyAsync(out, OUTb, nOUT * sizeof(float), hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : -1;
+}
+
+int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
                    hipStream_t st) {
   const int Lm = std::max(L0, Ld);
   const size_t BL0 = (size_t)B * L0, BLm = (size_t)B * std::max(Lm, S);
-  // workspace: E0 | X | QKV | CTX | HID | ENC | XD | QC
+  // workspace: E0 | X | QKV | CTX | HID | ENC | XD | QC | (graph inputs / output)
   const size_t nE0 = BL0 * D, nX = BL0 * D, nQKV = BLm * 3 * HE, nCTX = BLm * HE,
-               nHID = BLm * std::max(dff, D), nENC = (size_t)B * S * D, nXD = (size_t)B * Ld * D,
-               nQC = (size_t)B * Ld * HE;
-  const size_t need = nE0 + nX + nQKV + nCTX + nHID + nENC + nXD + nQC + 64;
-  if (need > ws_n) {
-    if (ws && hipFree(ws) != hipSuccess) return -1;
-    ws = nullptr;
-    if (hipMalloc((void**)&ws, need * sizeof(float)) != hipSuccess) return -1;
-    ws_n = need;
-  }
+               nHID = BLm * std::max(dff, D), nENC = (size_t)B * S * D, nXD = (size_t)B * Ld * D;
   float* E0 = ws;
   float* X = E0 + nE0;
   float* QKV = X + nX;
