@@ -105,19 +105,24 @@ def cpu_baseline(batch: int = 512, reps: int = 5):
 
 
 def load_traffic(profile_dir, kernel):
-    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary (None if the summary
-    was collected on another kernel variant), and the file it came from."""
-    path = os.path.join(profile_dir, "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None, None
-    try:
-        with open(path) as f:
-            d = json.load(f)
+    """HBM bytes per launch of `kernel` from the newest round's committed rocprofv3 PMC summary
+    (profiles/rNN/pmc_traffic.json; None if it was collected on another kernel variant), and the file
+    it came from."""
+    rounds = sorted((d for d in os.listdir(profile_dir) if d.startswith("r") and d[1:].isdigit()),
+                    reverse=True) if os.path.isdir(profile_dir) else []
+    for r in rounds:
+        path = os.path.join(profile_dir, r, "pmc_traffic.json")
+        if not os.path.exists(path):
+            continue
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            return None, None
         if kernel not in (d.get("kernel") or ""):
             return None, None
         return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
-    except (OSError, ValueError):
-        return None, None
+    return None, None
 
 
 def parse_args(argv=None):
