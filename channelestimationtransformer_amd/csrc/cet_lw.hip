@@ -18,6 +18,10 @@
 #include "cet_lw.h"
 
 namespace cet {
+bool ensure_lds_attr(const void* kern);   // cet_api.cpp
+}
+
+namespace cet {
 namespace lw {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -421,14 +425,8 @@ int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStre
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 int prepare_attention() {
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(lw_attention), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return -1;
-    attr = true;
-  }
-  return 0;
+  // once per (device, kernel), thread-safe (cet_api.cpp)
+  return cet::ensure_lds_attr(reinterpret_cast<const void*>(lw_attention)) ? 0 : -1;
 }
 int launch_attention(const AttnOp& op, int B, hipStream_t st) {
   if (op.LQ > LW_LMAX || op.LK > LW_LMAX) return -3;
