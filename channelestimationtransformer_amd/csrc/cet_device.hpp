@@ -53,7 +53,19 @@ __device__ __forceinline__ bf16x8 cvt8(const f32x4& lo, const f32x4& hi) {
   const f32x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_convertvector(v, bf16x8);
 }
-__device__ __forceinline__ bf16x4 cvt4(const f32x4& v) { return __builtin_convertvector(v, bf16x4); }
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+// 4-wide as two 2-wide conversions: a 4-wide convertvector is scalarised into four single-value
+// v_cvt_pk_bf16_f32 plus two v_perm_b32 (6 VALU); this is two v_cvt_pk_bf16_f32
+__device__ __forceinline__ bf16x4 cvt4(const f32x4& v) {
+#ifdef CET_CVT4_VEC
+  return __builtin_convertvector(v, bf16x4);
+#else
+  const bf16x2 a = __builtin_convertvector((f32x2{v[0], v[1]}), bf16x2);
+  const bf16x2 b = __builtin_convertvector((f32x2{v[2], v[3]}), bf16x2);
+  return __builtin_bit_cast(bf16x4, (u32x2{__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b)}));
+#endif
+}
 
 // XOR-butterfly reductions across the lane axis.  The 16- and 32-lane exchanges use gfx950's
 // v_permlane16_swap / v_permlane32_swap (one VALU op, no LDS); with both operands = v the two

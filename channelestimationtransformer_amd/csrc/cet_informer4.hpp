@@ -121,15 +121,22 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // 16-byte lane fragments per n-tile at K = 128
   // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles
-  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
-                    uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
-                    int mix, int call, float* attn_out) {
-    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+  auto head_io = [&](const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk, uint32_t Wv, GemmDesc dq,
+                     GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal, int mix, float* attn_out) {
     HeadIO<P> io;
     io.xq = Xq; io.xkv = Xkv; io.ctx = CTXI; io.wq = Wq; io.wk = Wk; io.wv = Wv;
     io.dq = dq; io.dk = dk; io.dv = dv;
     io.LQ = LQ; io.LK = LK; io.prob = prob; io.causal = causal; io.mix = mix; io.u = LQ;
     io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = attn_out; io.m_dbg = nullptr;
+    io.st = nullptr;
+    return io;
+  };
+  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles
+  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
+                    uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
+                    int mix, int call, float* attn_out) {
+    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
     io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
     if (call >= 0) {
       const AttnCall& c = PL.calls[call];
@@ -303,6 +310,16 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 #else
     for (int l = 0; l < PL.d_layers; ++l) {
 #endif
+#ifndef CET_NO_CROSS_HOIST
+      // cross-attention K/V of this layer (encoder-stack output only): projected before the
+      // self-attention, so their weight fetch overlaps it instead of following it (123.4 vs 124.3 us,
+      // profiles/r02/ab_cross_hoist.log)
+      const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
+      const HeadIO<P> cio = head_io(XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0), part_of(ckv, 0),
+                                    part_of(ckv, 128), Ld, S, 0, 0, 0, nullptr);
+      AF<PP> CK[NMS], CV[NMS];
+      project_kv<P, NMS>(cio, M, w, CK, CV);
+#endif
       {
         // masked self-attention with the mix scramble (model.py:211-222)
         const GemmDesc q = DLD.qkv;
@@ -317,9 +334,13 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       __syncthreads();
       {
         // cross-attention: FullAttention over the encoder-stack output, mix=False
+#ifndef CET_NO_CROSS_HOIST
+        attention_head<P, NMD, NMS, true>(cio, M, w, CK, CV);
+#else
         const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
         attend(IC<NMD>{}, IC<NMS>{}, XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
                part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
+#endif
       }
       const WPre<P, 4> pco = prefetch_res<P, 4>(M, DLD.co);
       __syncthreads();

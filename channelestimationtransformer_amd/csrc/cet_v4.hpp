@@ -704,8 +704,47 @@ struct HeadIO {
   unsigned long long* st;     // diagnostics: sub-phase s_memtime stamps of head 0, or nullptr
 };
 
-template <int PD, int MQ = MT, int MK = MT>
-__device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h) {
+// K and V tiles of head h from the key/value rows (attn.py:195-199): Kᵀ = Wk_h·Xᵀ as the A fragments
+// of Sᵀ = K·Qᵀ, V = X·Wv_hᵀ as the A fragments of Oᵀ = Vᵀ·Pᵀ.
+template <int PD, int MK>
+__device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, int h, AF<plain_of<PD>()> (&Kf)[MK],
+                                           AF<plain_of<PD>()> (&Vf)[MK]) {
+  constexpr int PA = plain_of<PD>();
+  const int lane = lane_op();
+  const int col = lane & 15, g = lane >> 4;
+  const int nkt = (io.LK + 15) >> 4;
+  const int fq = 16 * h + 4 * g;
+  const int kq = g * 8;
+  WF<PD> wk[4], wv[4];
+  load_frags<PD, 4>(m, io.wk, h, wk);
+  load_frags<PD, 4>(m, io.wv, h, wv);
+  f32x4 sk, bk;
+  epi_vecs(m, io.dk, fq, sk, bk);
+  const float sv = io.dv.scale != NONE ? pload1(m, io.dv.scale, 16 * h + col) : 1.f;
+  const float bv = io.dv.bias != NONE ? pload1(m, io.dv.bias, 16 * h + col) : 0.f;
+#pragma unroll
+  for (int mt = 0; mt < MK; ++mt) {
+    Kf[mt] = AF<PA>{};
+    Vf[mt] = AF<PA>{};
+    if (mt < nkt) {
+      f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = k;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const XF<PD> bx = io.xkv.ld(mt * 16 + col, ks * 32 + kq);
+        k = mma<PD>(wk[ks], bx, k);
+        v = mma_xw<PD>(bx, wv[ks], v);
+      }
+      Kf[mt] = split4<PA>(k * sk + bk);
+      Vf[mt] = split4<PA>(v * sv + bv);
+    }
+  }
+}
+
+// EXTKV: the K/V tiles come from the caller (kin / vin, project_kv) instead of being projected here.
+template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false>
+__device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
+                                               const AF<plain_of<PD>()>* kin = nullptr,
+                                               const AF<plain_of<PD>()>* vin = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -722,39 +761,36 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
   const int fq = 16 * h + 4 * g;
   const int kq = g * 8;
   AF<PA> Kf[MK], Vf[MK];
-  {
-    // pass 1: K and V tiles from the key/value rows
-    WF<PD> wk[4], wv[4];
-    load_frags<PD, 4>(m, io.wk, h, wk);
-    load_frags<PD, 4>(m, io.wv, h, wv);
-    f32x4 sk, bk;
-    epi_vecs(m, io.dk, fq, sk, bk);
-    const float sv = io.dv.scale != NONE ? pload1(m, io.dv.scale, 16 * h + col) : 1.f;
-    const float bv = io.dv.bias != NONE ? pload1(m, io.dv.bias, 16 * h + col) : 0.f;
+  // single-tile heads (the decoder's, and the last encoder layer's): few live registers, so the Q
+  // weights could be requested with the K/V weights (one L2 round trip instead of two in sequence);
+  // measured slower (126.5 vs 124.3 us, profiles/r02/ab_cross_hoist.log), so off unless CET_EARLYQ1
+#ifdef CET_EARLYQ1
+  constexpr bool EARLYQ = MQ == 1 && MK == 1;
+#else
+  constexpr bool EARLYQ = false;
+#endif
+  WF<PD> wq[4];
+  f32x4 sq, bq;
+  if constexpr (EARLYQ) {
+    load_frags<PD, 4>(m, io.wq, h, wq);
+    epi_vecs(m, io.dq, fq, sq, bq);
+  }
+  if constexpr (EXTKV) {
 #pragma unroll
     for (int mt = 0; mt < MK; ++mt) {
-      Kf[mt] = AF<PA>{};
-      Vf[mt] = AF<PA>{};
-      if (mt < nkt) {
-        f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = k;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const XF<PD> bx = io.xkv.ld(mt * 16 + col, ks * 32 + kq);
-          k = mma<PD>(wk[ks], bx, k);
-          v = mma_xw<PD>(bx, wv[ks], v);
-        }
-        Kf[mt] = split4<PA>(k * sk + bk);
-        Vf[mt] = split4<PA>(v * sv + bv);
-      }
+      Kf[mt] = kin[mt];
+      Vf[mt] = vin[mt];
     }
+  } else {
+    project_kv<PD, MK>(io, m, h, Kf, Vf);
   }
   SUB(1);
   // Q tiles are projected where they are consumed (per query tile in M, per selected tile in the
   // softmax): wq and its epilogue vectors are the only Q state that lives
-  WF<PD> wq[4];
-  load_frags<PD, 4>(m, io.wq, h, wq);
-  f32x4 sq, bq;
-  epi_vecs(m, io.dq, fq, sq, bq);
+  if constexpr (!EARLYQ) {
+    load_frags<PD, 4>(m, io.wq, h, wq);
+    epi_vecs(m, io.dq, fq, sq, bq);
+  }
   auto project_q = [&](int row) __attribute__((always_inline)) {
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
