@@ -29,8 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
-KERNEL_NAMES = {1: "cet::informer_forward<64>",
-                3: "cet::v3::informer_forward_v3<64, false, false>",
+KERNEL_NAMES = {3: "cet::v3::informer_forward_v3<64, false, false>",
                 4: "cet::v4::informer_forward_v4<64, false, 0>"}
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
@@ -137,7 +136,7 @@ def parse_args(argv=None):
     ap.add_argument("--snr", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=4,
-                    help="fused-kernel generation (1: LDS-resident, 3/4: 8-wave register-resident)")
+                    help="fused-kernel generation (3: round-1 kernel, 4: current; both 8-wave register-resident)")
     ap.add_argument("--sampler", choices=("device", "host"), default="device",
                     help="where the native ProbSparse draws run (identical streams; DESIGN §3.3)")
     ap.add_argument("--nmse", choices=("fused", "separate"), default="fused",

@@ -134,7 +134,7 @@ struct cet_engine {
   std::vector<std::string> order;
   bool dirty = true;
   bool uploaded = false;
-  int variant = 4;   // fused-kernel generation (CET_KERNEL=v1 / v3 select the older kernels)
+  int variant = 4;   // fused-kernel generation (CET_KERNEL=v3 selects the round-1 kernel)
   // shapes outside the fused kernels (d_model != 128, n_heads != 8, d_ff > 128, ...): the layer-wise
   // engine (cet_lw.hip), fp32 on the f32 MFMA, one launch per operator
   bool generic = false;
@@ -1272,7 +1272,7 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   e->icfg = *cfg;
   e->generic = !fused_supported(*cfg) || std::getenv("CET_LAYERWISE") != nullptr;
   if (const char* v = std::getenv("CET_KERNEL"))
-    e->variant = std::strcmp(v, "v1") == 0 ? 1 : (std::strcmp(v, "v3") == 0 ? 3 : 4);
+    e->variant = std::strcmp(v, "v3") == 0 ? 3 : 4;
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
   const auto& c = *cfg;
@@ -1445,7 +1445,6 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen) {
 static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   const InformerPlan& p = e->ip;
   switch (e->variant) {
-    case 1: return cet_launch_informer(&a, e->icfg.d_ff, p.lds_bytes, st);
     case 4: {
       InformerArgs b = a;
       b.wlo = (uint32_t)(e->wblob.size() * 2);
@@ -1538,8 +1537,7 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     a.dbg = e->dbg;
     a.B = B;
     const int tk = timing_mark(e, st);
-    rc = e->variant == 1 ? cet_launch_transformer(&a, e->tcfg.d_ff, e->tp.lds_bytes, st)
-                         : cet_launch_transformer_v4(&a, e->tcfg.d_ff, e->tp.lds4_bytes, st);
+    rc = cet_launch_transformer_v4(&a, e->tcfg.d_ff, e->tp.lds4_bytes, st);
     if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
     if (rc) return fail(CET_E_HIP, std::string("transformer launch failed: ") + hipGetErrorString(hipGetLastError()));
     return CET_OK;
@@ -1728,10 +1726,10 @@ int cet_set_sampler(cet_engine* e, int on_host) {
 
 int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
-  if (variant != 1 && variant != 3 && variant != 4) return fail(CET_E_INVALID, "variant must be 1, 3 or 4");
+  if (variant != 3 && variant != 4)
+    return fail(CET_E_INVALID, "variant must be 3 or 4 (the round-1 LDS-resident kernel 1 is retired)");
   if (variant != e->variant) e->dirty = true;   // the precision resolution depends on the kernel
-  if (e->kind != 0 && variant != 1 && variant != 4)
-    return fail(CET_E_INVALID, "the Transformer engine has variants 4 (default) and 1");
+  if (e->kind != 0 && variant != 4) return fail(CET_E_INVALID, "the Transformer engine has variant 4 only");
   e->variant = variant;
   return CET_OK;
 }

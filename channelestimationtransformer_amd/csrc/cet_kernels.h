@@ -78,7 +78,6 @@ bool ensure_lds_attr(const void* kern);
 
 }  // namespace cet
 
-extern "C" int cet_launch_informer(const cet::InformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
                                        uint8_t* tab_out, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, int xdec_early,
@@ -86,7 +85,6 @@ extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int l
 extern "C" int cet_launch_informer_v4(const cet::InformerArgs* a, int prec, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
-extern "C" int cet_launch_transformer(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_nmse_split(const float* pred, const float* label, int B, int T, int F, float* acc,
                                      float* last, int accumulate, double* sums, hipStream_t stream);

@@ -152,7 +152,7 @@ class Engine:
         check(lib.cet_set_sampler(self._h, int(bool(on_host))), "cet_set_sampler")
 
     def set_variant(self, variant: int) -> None:
-        """Fused-kernel generation: 4 (default), 3 (bf16-only predecessor) or 1 (LDS-resident)."""
+        """Fused-kernel generation: 4 (default) or 3 (its bf16-only predecessor)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
 
     PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3}

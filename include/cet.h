@@ -117,8 +117,9 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen);
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
 
 /* Select the fused-kernel generation of an Informer engine: 4 (default: 8-wave register-resident,
- * two sequences per CU, precision policies), 3 (its bf16-only predecessor) or 1 (LDS-resident, one
- * sequence per CU).  CET_KERNEL=v1 / v3 in the environment selects 1 / 3 at creation. */
+ * two sequences per CU, precision policies) or 3 (its bf16-only predecessor).  CET_KERNEL=v3 in the
+ * environment selects 3 at creation.  Transformer engines have generation 4 only.  (Generation 1, the
+ * round-1 LDS-resident kernel, is retired: CET_E_INVALID.) */
 int cet_set_variant(cet_engine* e, int variant);
 
 /* Operand precision of the v4 kernel's dense layers (Informer engines):

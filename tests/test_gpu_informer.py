@@ -455,9 +455,9 @@ def test_nmse_split_kernel(shape):
     np.testing.assert_allclose(acc.cpu().numpy(), 3 * ref_split(p, y), rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4])
+@pytest.mark.parametrize("variant", [3, 4])
 def test_kernel_variants_agree_with_oracle(variant):
-    """Both fused-kernel generations (LDS-resident v1, register-resident v3) meet the bar."""
+    """Both register-resident fused-kernel generations (v3, v4) meet the bar."""
     _gpu()
     from channelestimationtransformer_amd.dataset import make_batch
     from engine_util import model_for, run_engine

@@ -114,8 +114,6 @@ def main():
     runs = [
         ("C3 Transformer (full attention, no distil), N=3", lambda: transformer(dev), 512, transformer_flops(),
          dict(variant=4), "bf16"),
-        ("C3 Transformer, v1 LDS-resident kernel", lambda: transformer(dev), 512, transformer_flops(),
-         dict(variant=1), "bf16"),
         ("C5 InformerStackLSQ 8-bit weights, bf16 activations", lambda: informer(dev, [4], "prob", 8), 1024,
          informer_flops(), dict(precision="bf16"), "bf16"),
         ("C5 InformerStackLSQ 8-bit weights, fp8 e4m3 activations", lambda: informer(dev, [4], "prob", 8), 1024,
