@@ -70,3 +70,36 @@ def test_trained_mimo_checkpoint_drops_into_the_engine():
     eng.load_state_dict({k: v.numpy() for k, v in m.state_dict().items()})
     assert eng.precision() == "fp32-layerwise"
     assert [L for _, L in eng.attns_layout()] == [25, 13, 7, 4, 12, 6, 3]
+
+
+def test_weight_staleness_check_is_cheap_and_complete():
+    """The per-forward check that decides whether the engine's packed weights are stale (informer.py
+    _version) sees in-place edits, load_state_dict and parameter re-assignment, ignores unrelated module
+    construction, and does not walk the state_dict on every call (the TimingAnalysis batch-1 harness
+    times the model call with its Python dispatch)."""
+    import time
+
+    m = _model().eval()
+    v0 = m._version()
+    t = time.perf_counter()
+    for _ in range(200):
+        assert m._version() == v0
+    per_call = (time.perf_counter() - t) / 200
+    t = time.perf_counter()
+    for _ in range(20):
+        m.state_dict()
+    walk = (time.perf_counter() - t) / 20
+    assert per_call < walk / 5, (per_call, walk)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        m.projection.weight.add_(1.0)
+    v1 = m._version()
+    assert v1 != v0
+    m.load_state_dict(sd)
+    v2 = m._version()
+    assert v2 != v1
+    m.projection.bias = torch.nn.Parameter(m.projection.bias.detach().clone(), requires_grad=False)
+    v3 = m._version()
+    assert v3 != v2
+    torch.nn.Linear(3, 3)   # another module's registrations do not invalidate this one
+    assert m._version() == v3
