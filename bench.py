@@ -332,7 +332,7 @@ def main(argv=None):
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # the CPU leg: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(B)
         print(json.dumps(res), flush=True)
     if dist:
