@@ -811,24 +811,6 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       const uint2* crow = reinterpret_cast<const uint2*>(io.cnt + (size_t)q * io.cnt_stride + g * 24);
       const uint2 c01 = crow[0], c23 = crow[1], c45 = crow[2];
       const uint32_t cws[MT] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
-#ifdef CET_M2CHAIN
-      // two independent (sum, max) chains over even / odd key tiles: half the dependent VALU depth
-      float sc[2] = {0.f, 0.f}, mc[2] = {NEG_INF, NEG_INF};
-#pragma unroll
-      for (int kt = 0; kt < MK; ++kt) {
-        if (kt < nkt) {
-          const f32x4 s = mma16<PA>(Kf[kt], qf, f32x4{0.f, 0.f, 0.f, 0.f});
-          const uint32_t cw = cws[kt];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float cf = (float)((cw >> (8 * r)) & 0xffu);
-            sc[kt & 1] = fmaf(cf, s[r], sc[kt & 1]);
-            mc[kt & 1] = fmaxf(mc[kt & 1], cf != 0.f ? s[r] : NEG_INF);
-          }
-        }
-      }
-      float sum = sc[0] + sc[1], mx = fmaxf(mc[0], mc[1]);
-#else
       float sum = 0.f, mx = NEG_INF;
 #pragma unroll
       for (int kt = 0; kt < MK; ++kt) {
@@ -848,7 +830,6 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
           }
         }
       }
-#endif
       sum = xor_sum(sum, 16);
       sum = xor_sum(sum, 32);
       mx = xor_max(mx, 16);
