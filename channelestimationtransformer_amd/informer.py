@@ -30,7 +30,24 @@ from .weights import synthetic_state_dict
 
 
 def build_param_tree(root: nn.Module, entries, values=None) -> None:
-    """Create nested sub-modules so that ``root.state_dict()`` has exactly the schema's keys."""
+    """Create nested sub-modules so that ``root.state_dict()`` has exactly the schema's keys.
+
+    Every parameter and buffer is a view of one flat float32 (or int64) tensor: views share their base's
+    version counter, so an in-place edit of any of them — ``load_state_dict`` included — moves
+    ``root._flat[i]._version`` and the per-forward staleness check is O(1) (:meth:`_EngineModule._version`)."""
+    def numel(shape):
+        n = 1
+        for d in shape:
+            n *= int(d)
+        return n
+
+    sizes = {False: 0, True: 0}
+    for _, shape, kind in entries:
+        sizes[kind == "bn_nbt"] += numel(shape)
+    flat = {False: torch.zeros(max(sizes[False], 1), dtype=torch.float32),
+            True: torch.zeros(max(sizes[True], 1), dtype=torch.int64)}
+    offs = {False: 0, True: 0}
+    owned = {}
     for key, shape, kind in entries:
         *path, leaf = key.split(".")
         mod = root
@@ -38,14 +55,24 @@ def build_param_tree(root: nn.Module, entries, values=None) -> None:
             if not hasattr(mod, p) or not isinstance(getattr(mod, p), nn.Module):
                 mod.add_module(p, nn.Module())
             mod = getattr(mod, p)
+        isint = kind == "bn_nbt"
+        n = numel(shape)
+        view = flat[isint][offs[isint]:offs[isint] + n].view(tuple(shape))
+        offs[isint] += n
         if values is not None and key in values:
-            t = torch.as_tensor(np.asarray(values[key]))
-        else:
-            t = torch.zeros(shape, dtype=torch.int64 if kind == "bn_nbt" else torch.float32)
+            view.copy_(torch.as_tensor(np.asarray(values[key])).reshape(view.shape))
         if kind in ("pe", "bn_rm", "bn_rv", "bn_nbt"):
-            mod.register_buffer(leaf, t.clone())
+            mod.register_buffer(leaf, view)
+            t = getattr(mod, leaf)
         else:
-            mod.register_parameter(leaf, nn.Parameter(t.clone(), requires_grad=False))
+            t = nn.Parameter(view, requires_grad=False)
+            mod.register_parameter(leaf, t)
+        owned[id(t)] = t
+    with torch.no_grad():
+        for f in flat.values():
+            f.add_(0)   # one version step after the fills, so a fresh tree never matches a stale record
+    root._flat = (flat[False], flat[True])
+    root._owned = owned
 
 
 # Every parameter / buffer / sub-module registration anywhere in the process bumps this counter (torch's
@@ -90,8 +117,13 @@ class _EngineModule(nn.Module):
             if old is None or len(old) != len(tensors) or any(a is not b for a, b in zip(old, tensors)):
                 self._tensors = tensors
                 self._tensor_set = getattr(self, "_tensor_set", 0) + 1   # a different set: force a re-sync
+                owned = getattr(self, "_owned", {})
+                # tensors build_param_tree made are views of self._flat (one shared version counter each);
+                # anything assigned since is checked on its own
+                self._foreign = tuple(t for t in tensors if owned.get(id(t)) is not t)
             self._tensors_at = _REGISTRATIONS[0]
-        return (self._tensor_set, id(self), tuple(t._version for t in self._tensors))
+        return (self._tensor_set, id(self), tuple(f._version for f in getattr(self, "_flat", ())),
+                tuple(t._version for t in self._foreign))
 
     def engine(self, device) -> Engine:
         device = torch.device(device)

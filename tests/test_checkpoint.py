@@ -101,5 +101,13 @@ def test_weight_staleness_check_is_cheap_and_complete():
     m.projection.bias = torch.nn.Parameter(m.projection.bias.detach().clone(), requires_grad=False)
     v3 = m._version()
     assert v3 != v2
+    with torch.no_grad():
+        m.projection.bias.add_(1.0)       # an in-place edit of a re-assigned (non-flat) parameter
+    v4 = m._version()
+    assert v4 != v3
+    with torch.no_grad():
+        m.decoder.norm.weight.mul_(2.0)   # and of one still backed by the flat tensor
+    v5 = m._version()
+    assert v5 != v4
     torch.nn.Linear(3, 3)   # another module's registrations do not invalidate this one
-    assert m._version() == v3
+    assert m._version() == v5
