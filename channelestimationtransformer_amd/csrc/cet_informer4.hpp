@@ -120,7 +120,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   STAMP();
 
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // 16-byte lane fragments per n-tile at K = 128
-  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles
+  // the per-head operands of one attention call (AttentionLayer, attn.py:178-209)
   auto head_io = [&](const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk, uint32_t Wv, GemmDesc dq,
                      GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal, int mix, float* attn_out) {
     HeadIO<P> io;
