@@ -14,3 +14,7 @@ timeout -k 10 400 python tools/bench_configs.py > "$O/configs.jsonl" 2> "$O/conf
 cat "$O/configs.jsonl" | cut -c1-220
 timeout -k 10 200 python tools/stamps.py 512 > "$O/stamps_b512.txt" 2> "$O/stamps.err" || exit 1
 head -3 "$O/stamps_b512.txt"
+timeout -k 10 300 python -m channelestimationtransformer_amd.sweep --batches 200 > "$O/sweep_200batches.jsonl" 2> "$O/sweep.err" || exit 1
+cut -c1-200 "$O/sweep_200batches.jsonl"
+timeout -k 10 600 python -m channelestimationtransformer_amd.latency --sweep --reps 300 > "$O/latency_sweep.jsonl" 2> "$O/latency.err" || exit 1
+head -2 "$O/latency_sweep.jsonl" | cut -c1-200
