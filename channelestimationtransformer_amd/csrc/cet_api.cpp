@@ -184,6 +184,11 @@ struct cet_engine {
   int tab_cur = 0;
   bool tab_ready = false;
   unsigned* d_ticket = nullptr;
+  // v4 encoder split (launch_fused): exchange image rows [B][S][RS / 8] and per-sequence arrival counts
+  uint64_t* d_enc_xchg = nullptr;
+  size_t enc_xchg_n = 0;
+  unsigned* d_enc_count = nullptr;
+  int enc_count_n = 0;
   float2* d_nmse_part = nullptr;   // fused NMSE: per-sequence partials [B][pred_len]
   size_t nmse_part_n = 0;
   static constexpr int PREP_MIN_B = 64;   // below this the first finisher has no slack to hide in
@@ -225,6 +230,8 @@ struct cet_engine {
     for (auto* t : d_tab)
       if (t) (void)hipFree(t);
     if (d_ticket) (void)hipFree(d_ticket);
+    if (d_enc_xchg) (void)hipFree(d_enc_xchg);
+    if (d_enc_count) (void)hipFree(d_enc_count);
     if (d_nmse_part) (void)hipFree(d_nmse_part);
     if (h_mt) (void)hipHostFree(h_mt);
     for (auto* h : h_lwidx)
@@ -1448,6 +1455,31 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
     case 4: {
       InformerArgs b = a;
       b.wlo = (uint32_t)(e->wblob.size() * 2);
+      b.enc_split = 0;
+      b.enc_xchg = nullptr;
+      b.enc_count = nullptr;
+      // encoder split: the encoders of a stack are independent until the decoder, so at small batches
+      // each runs on its own workgroup (bf16 policy, no ProbSparse draws, production outputs only, the
+      // whole grid resident at two workgroups per CU)
+      static const bool no_split = std::getenv("CET_NO_ENC_SPLIT") != nullptr;
+      if (!no_split && e->prec == 0 && p.n_enc > 1 && p.n_calls == 0 && !a.attns && !a.dbg && !a.stamps &&
+          (int64_t)a.B * p.n_enc <= 512) {
+        const size_t words = (size_t)a.B * p.S * (v4_rs(0) / 8);
+        if (words > e->enc_xchg_n) {
+          if (e->d_enc_xchg) HIP_TRY(hipFree(e->d_enc_xchg));
+          HIP_TRY(hipMalloc((void**)&e->d_enc_xchg, words * sizeof(uint64_t)));
+          e->enc_xchg_n = words;
+        }
+        if (a.B > e->enc_count_n) {
+          if (e->d_enc_count) HIP_TRY(hipFree(e->d_enc_count));
+          HIP_TRY(hipMalloc((void**)&e->d_enc_count, (size_t)a.B * sizeof(unsigned)));
+          HIP_TRY(hipMemsetAsync(e->d_enc_count, 0, (size_t)a.B * sizeof(unsigned), st));   // re-armed by the kernel
+          e->enc_count_n = a.B;
+        }
+        b.enc_split = p.n_enc;
+        b.enc_xchg = e->d_enc_xchg;
+        b.enc_count = e->d_enc_count;
+      }
       const bool replay = a.mt_in && !a.cnt;
       return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);
     }

@@ -49,7 +49,7 @@ __device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
 
 // P: precision of the dense (LSQ-quantisable) layers; DIAG: the instance that honours the optional
 // outputs (attns maps, activation dumps, phase stamps) — the production instance compiles them out.
-template <int DFF, bool DIAG, int P>
+template <int DFF, bool DIAG, int P, bool SPLIT = false>
 __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(plan))
@@ -58,7 +58,9 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   constexpr int PP = plain_of<P>();       // embedding / projection precision
   using G = Geo<P>;
   const Mem M{make_rsrc(a.weights), make_rsrc(a.params), a.wlo};
-  const int b = blockIdx.x;
+  const int nsplit = SPLIT ? PL.n_enc : 1;
+  const int b = SPLIT ? (int)blockIdx.x / nsplit : (int)blockIdx.x;
+  const int my_e = SPLIT ? (int)blockIdx.x - b * nsplit : -1;   // the one encoder of this workgroup
   if (b >= a.B) return;
   const int w = wave_id();
 #ifndef CET_NO_SETPRIO
@@ -166,7 +168,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
-    if (e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);   // CTX was reused by encoder e-1
+    if (SPLIT && e != my_e) continue;   // the entry staging of x_enc is still intact for it
+    if (!SPLIT && e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);   // CTX was reused by encoder e-1
     __syncthreads();
     // ---- DataEmbedding (embed.py:132-135) on the EncoderStack window x[:, -L:] (encoder.py:95-106)
     int L = L0 >> e;
@@ -282,6 +285,36 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   // ================================ decoder (decoder.py:43-56), instantiated for its compile-time
   // tile count (dec_len ≤ 48); the staged decoder input is in XDEC
   const int S = PL.S;
+  if constexpr (SPLIT) {
+    // ---- publish this encoder's rows of the stack output (write-through, like the NMSE partials),
+    //      count the arrival; the last of the sequence's workgroups fetches the other rows and goes on
+    constexpr int RW = G::RS / 8;   // u64 words per image row
+    uint64_t* xchg = a.enc_xchg + (size_t)b * S * RW;
+    const uint64_t* enc64 = reinterpret_cast<const uint64_t*>(ENC.base);
+    {
+      const int r0 = PL.enc_row_off[my_e], n = PL.enc_rows[my_e] * RW;
+      for (int i = threadIdx.x; i < n; i += NTHREADS)
+        __hip_atomic_store(xchg + r0 * RW + i, enc64[r0 * RW + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* tk = reinterpret_cast<unsigned*>(lds + v4_scr(P));
+    if (threadIdx.x == 0) {
+      const unsigned t = atomicAdd(a.enc_count + b, 1u);
+      if (t + 1u == (unsigned)nsplit) atomicExch(a.enc_count + b, 0u);   // re-arm for the next launch
+      *tk = t;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(*tk) + 1u != (unsigned)nsplit) return;   // uniform: the whole workgroup
+    uint64_t* encw = reinterpret_cast<uint64_t*>(ENC.base);
+    for (int e = 0; e < nsplit; ++e) {
+      if (e == my_e) continue;
+      const int r0 = PL.enc_row_off[e], n = PL.enc_rows[e] * RW;
+      for (int i = threadIdx.x; i < n; i += NTHREADS)
+        encw[r0 * RW + i] = __hip_atomic_load(xchg + r0 * RW + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
   if (xdec_off < 0) {   // no room to keep it since entry: stage it now (into CTX, free after the encoder)
     stage(a.x_dec + (size_t)b * Ld * C, XDEC, Ld, C, CS);
     __syncthreads();
@@ -500,10 +533,10 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 }
 
 // X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
-template <int DFF, bool DIAG, int P>
+template <int DFF, bool DIAG, int P, bool SPLIT = false>
 __global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
     informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
-  informer_forward_v4_body<DFF, DIAG, P>(a, plan);
+  informer_forward_v4_body<DFF, DIAG, P, SPLIT>(a, plan);
 }
 
 template <int P>
@@ -512,13 +545,25 @@ int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream)
   const bool diag = a->attns || a->dbg || a->stamps;
   using K = void (*)(InformerArgs, const InformerPlan*);
   K kern = nullptr;
-  if (dff == 64) kern = diag ? informer_forward_v4<64, true, P> : informer_forward_v4<64, false, P>;
+  const bool split = a->enc_split != 0;
+  if (split) {
+    // encoder split: bf16 policy, production instance only (the launcher checks the plan's conditions)
+    if constexpr (P == P_BF16) {
+      if (diag) return -3;
+      if (dff == 64) kern = informer_forward_v4<64, false, P, true>;
+      else if (dff == 128) kern = informer_forward_v4<128, false, P, true>;
+      else return -3;
+    } else {
+      return -3;
+    }
+  } else if (dff == 64) kern = diag ? informer_forward_v4<64, true, P> : informer_forward_v4<64, false, P>;
   else if (dff == 128) kern = diag ? informer_forward_v4<128, true, P> : informer_forward_v4<128, false, P>;
   else return -3;
   if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
   InformerArgs args = *a;
   args.lds_bytes = lds_bytes;
-  hipLaunchKernelGGL(kern, dim3(a->B), dim3(NTHREADS), lds_bytes, stream, args, a->plan);
+  const unsigned grid = (unsigned)a->B * (split ? (unsigned)a->enc_split : 1u);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHREADS), lds_bytes, stream, args, a->plan);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -32,6 +32,12 @@ struct InformerArgs {
   float2* nmse_part;          // [B][pred_len] per-sequence (Σ(x−x̂)², Σx̂²), written write-through (sc1)
   float* nmse_acc;            // [pred_len] ratio, accumulated (+=) by the last workgroup, or null
   double* nmse_sums;          // [2][pred_len] global sums (overwritten) by the last workgroup, or null
+  // v4 encoder split (stacks, no ProbSparse calls, small batches): workgroup (b, e) runs encoder e of
+  // sequence b, publishes its rows of the stack output, and the last of a sequence's workgroups to finish
+  // runs the decoder; the others exit
+  int enc_split;              // 0 / 1
+  uint64_t* enc_xchg;         // [B][S rows][row stride / 8] bf16 stack-output image rows
+  unsigned* enc_count;        // [B] arrivals (the last arrival re-arms it)
 };
 
 // device channel pipeline (cet_data.hip)
