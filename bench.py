@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
 KERNEL_NAMES = {3: "cet::v3::informer_forward_v3<64, false, false>",
-                4: "cet::v4::informer_forward_v4<64, false, 0>"}
+                4: "cet::v4::informer_forward_v4<64, false, 0, false>"}
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
            n_heads=8, e_layers=[4], d_layers=3, d_ff=64, dropout=0.05, attn="prob", embed="fixed",
