@@ -409,6 +409,34 @@ def test_encoder_split_small_batches_vs_oracle(B):
     assert rel_nmse(out[rows], ref) < TOL
 
 
+@pytest.mark.parametrize("e_layers,B", [([3, 2, 1], 5), ([2, 2, 1, 1], 3), ([3, 2, 1], 170)])
+def test_encoder_split_deeper_stacks_vs_oracle(e_layers, B):
+    """The encoder split with three and four encoders per stack (seeded synthetic weights, attn="full")
+    against the float64 oracle; at B=170 the grid is 510 workgroups."""
+    _gpu()
+    from channelestimationtransformer_amd.dataset import make_batch
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+    from oracle.informer_np import InformerConfig, InformerOracle
+
+    dev = torch.device("cuda:0")
+    m = InformerStack(16, 16, 16, 90, 10, 5, 5, 128, 8, e_layers, 3, 64, 0.05, "full", "fixed", "gelu", False,
+                      True, dev)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(m._schema(), 3).items()})
+    m.eval()
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    orc = InformerOracle(InformerConfig(e_layers=tuple(e_layers), attn="full"), state)
+    xe, xd, _ = make_batch(B, seed=77 + B)
+    with torch.no_grad():
+        # the callers' 19-positional-argument call leaves output_attention on: (out, lazy attns)
+        res = m(torch.from_numpy(xe).to(dev), range(90), torch.from_numpy(xd).to(dev), range(15))
+    out = (res[0] if isinstance(res, tuple) else res).cpu().numpy()
+    rows = np.arange(B) if B <= 16 else np.r_[0:8, B - 8:B]
+    ref, _ = orc.forward(xe[rows], xd[rows], ())
+    assert np.isfinite(out).all()
+    assert rel_nmse(out[rows], ref) < TOL
+
+
 def test_attention_maps_materialised():
     _gpu()
     from engine_util import model_for, run_engine
