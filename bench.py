@@ -29,8 +29,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
-KERNEL_NAMES = {3: "cet::v3::informer_forward_v3<64, false, false>",
-                4: "cet::v4::informer_forward_v4<64, false, 0, false>"}
+KERNEL_NAMES = {4: "cet::v4::informer_forward_v4<64, false, 0, false>",
+                5: "cet::v5::informer_forward_v5<64, 0>"}
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
            n_heads=8, e_layers=[4], d_layers=3, d_ff=64, dropout=0.05, attn="prob", embed="fixed",
@@ -136,7 +136,7 @@ def parse_args(argv=None):
     ap.add_argument("--snr", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=4,
-                    help="fused-kernel generation (3: round-1 kernel, 4: current; both 8-wave register-resident)")
+                    help="fused-kernel generation (4: one sequence per workgroup, default; 5: two per workgroup)")
     ap.add_argument("--sampler", choices=("device", "host"), default="device",
                     help="where the native ProbSparse draws run (identical streams; DESIGN §3.3)")
     ap.add_argument("--nmse", choices=("fused", "separate"), default="fused",
@@ -235,16 +235,17 @@ def main(argv=None):
     lab = torch.from_numpy(lab_np).to(dev)
     out = torch.empty(B, T, 16, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    warm_sums = torch.zeros(2, T, dtype=torch.float64, device=dev)
-    sums = torch.zeros(args.steps, 2, T, dtype=torch.float64, device=dev)
+    all_sums = torch.zeros(args.steps + 1, 2, T, dtype=torch.float64, device=dev)   # row `steps`: warm-up
+    sums = all_sums[:args.steps]
+    fused_step = eng.bind_forward_nmse(xe, xd, out, lab, all_sums, stream)
 
     def step(k):
-        # forward + NMSE_Split of the batch: one launch (v4 fuses the reduction into its epilogue)
+        # forward + NMSE_Split of the batch: one launch (the kernel fuses the reduction into its epilogue)
         if args.nmse == "fused":
-            eng.forward_nmse(xe, xd, out, lab, None, sums[k] if k >= 0 else warm_sums, stream)
+            fused_step(k if k >= 0 else args.steps)
         else:
             eng.forward(xe, xd, out, None, stream)
-            nmse_split_sums(out, lab, sums[k] if k >= 0 else warm_sums, stream=stream)
+            nmse_split_sums(out, lab, all_sums[k if k >= 0 else args.steps], stream=stream)
 
     t_w = time.perf_counter()
     n_warm = 0
@@ -269,6 +270,8 @@ def main(argv=None):
     dt_rank = time.perf_counter() - t0
     kern_ms, launches = eng.timing_read()
     eng.timing(False)
+    path = eng.last_path()            # the fused kernel the timed steps launched
+    kernel_name = KERNEL_NAMES[5 if path == "v5" else 4]
 
     per_rank = [dt_rank]
     if dist:
@@ -302,7 +305,7 @@ def main(argv=None):
             parity = float(np.sum((a - r) ** 2) / np.sum(r ** 2))
         except Exception as exc:  # pragma: no cover - reported, not fatal
             parity = f"error: {exc}"
-        traffic, traffic_src = load_traffic(os.path.join(ROOT, "profiles"), KERNEL_NAMES[args.variant])
+        traffic, traffic_src = load_traffic(os.path.join(ROOT, "profiles"), kernel_name)
         res = {
             "metric": METRIC,
             "value": round(seqs / dt, 1),
@@ -317,7 +320,7 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (seeded Jakes channels, SNR %g dB; seeded synthetic weights)" % args.snr,
             "config": {"workload": WORKLOAD, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"dp{world}", "nmse": args.nmse},
+                       "parallelism": f"dp{world}", "nmse": args.nmse, "kernel_variant": args.variant},
             "world": world,
             "backend": "nccl" if world > 1 else None,
             "per_rank_ms_per_step": [round(t / args.steps * 1e3, 4) for t in per_rank],
@@ -328,7 +331,7 @@ def main(argv=None):
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": KERNEL_NAMES[args.variant], "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel": kernel_name, "kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }

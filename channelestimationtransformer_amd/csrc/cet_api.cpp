@@ -134,7 +134,11 @@ struct cet_engine {
   std::vector<std::string> order;
   bool dirty = true;
   bool uploaded = false;
-  int variant = 4;   // fused-kernel generation (CET_KERNEL=v3 selects the round-1 kernel)
+  int last_path = 0; // the fused kernel the last forward launched (CET_PATH_*), 0: none yet
+  int v5_min_b = 1;  // smallest batch v5 runs (CET_V5_MIN_B); smaller ones go to v4
+  bool enc_split_ok = true;   // v4 encoder split allowed (CET_NO_ENC_SPLIT at creation turns it off)
+  int variant = 4;   // fused-kernel generation: 4 (one sequence per workgroup, default) or 5 (two per
+                     // workgroup where the plan allows; CET_KERNEL=v5)
   // shapes outside the fused kernels (d_model != 128, n_heads != 8, d_ff > 128, ...): the layer-wise
   // engine (cet_lw.hip), fp32 on the f32 MFMA, one launch per operator
   bool generic = false;
@@ -486,7 +490,7 @@ int resolve_precision(cet_engine* e, float qmax, int* out) {
   const int Ld = c.label_len + c.out_len;
   const bool sparse_dec = c.attn_prob && u_part(c.factor, Ld) < Ld;
   int P = e->prec_req;
-  if (P < 0) P = (e->variant == 4 && (qmax > 256.f || sparse_dec)) ? 1 : 0;
+  if (P < 0) P = (qmax > 256.f || sparse_dec) ? 1 : 0;
   if (P == 2) {
     if (c.lsq_bits <= 0 || c.lsq_bits > 8)
       return fail(CET_E_INVALID, "fp8 activations need an LSQ engine of at most 8 bits (integer grid in e4m3 pairs)");
@@ -495,7 +499,6 @@ int resolve_precision(cet_engine* e, float qmax, int* out) {
   if (P == 0 && qmax > 256.f)
     return fail(CET_E_INVALID, "LSQ grid with |q| = " + std::to_string((int)qmax) +
                                    " > 256 is not exact in bf16; use the split-bf16 precision");
-  if (P != 0 && e->variant != 4) return fail(CET_E_INVALID, "precision modes need the v4 kernel");
   *out = P;
   return CET_OK;
 }
@@ -746,51 +749,12 @@ int build_informer(cet_engine* e) {
   const int LP = r16(std::max(c.seq_len, Ld));
   const int SP = r16(S);
   auto al = [](int x) { return (x + 15) & ~15; };
-  int o = 0;
-  p.lds_X = o; o = al(o + LP * XS * 4);
-  p.lds_Q = o; o = al(o + LP * BS * 2);
-  p.lds_K = o; o = al(o + LP * BS * 2);
-  p.vts = std::max(LP, SP) + 8;
-  p.lds_VT = o; o = al(o + DMODEL * p.vts * 2);
-  p.lds_ENC = o; o = al(o + SP * BS * 2);
-  p.lds_CTX = o; o = al(o + r16(Ld) * BS * 2);
-  p.lds_M = o; o = al(o + NHEAD * 96 * 4);
-  p.lds_SEL = o; o = al(o + NHEAD * 96 * 2);
-  p.lds_FLAG = o; o = al(o + NHEAD * 96);
-  p.lds_bytes = o;
   p.in_stride = c.enc_in + 4;
-  // v2: bf16 activation image | context/FFN hidden/staged input | stack output | LN partials | scratch
-  o = 0;
-  p.lds2_XB = o; o = al(o + LP * BS * 2);
-  p.lds2_CTX = o; o = al(o + std::max(LP * BS * 2, LP * p.in_stride * 4));
-  p.lds2_ENC = o; o = al(o + SP * BS * 2);
-  p.lds2_LN = o; o = al(o + LP * 8 * 4);
-  p.lds2_SCR = o; o = al(o + 4 * V2_SCR_FLOATS * 4);
   int max_cnt = 0;
   for (int k = 0; k < p.n_calls; ++k)
     if (p.calls[k].u < p.calls[k].LQ) max_cnt = std::max(max_cnt, r16(p.calls[k].LQ) * p.calls[k].cnt_stride);
-  p.lds2_CNT = o; o = al(o + max_cnt);
-  p.lds2_MT = o; o = al(o + 624 * 4);
-  p.lds2_bytes = o;
-  // v3: bf16 image | context/FFN hidden/staged input | stack output | 8 waves' attention scratch,
-  // aliased by the LayerNorm partials | multiplicity table | sampler state (≤ 80 KB: 2 per CU)
-  o = 0;
-  // (fixed layout, cet_plan.hpp V3L_*: only the stack output's size depends on the plan)
-  if (LMAX * p.in_stride * 4 > V3L_SCR - V3L_CTX || max_cnt > V3L_MT - V3L_CNT || LP > LMAX || (c.enc_in & 3))
-    return fail(CET_E_INVALID, "v3 LDS layout: staged input or multiplicity table exceeds its region");
-  p.lds3_XB = V3L_XB;
-  p.lds3_CTX = V3L_CTX;
-  p.lds3_SCR = V3L_SCR;
-  p.lds3_CNT = V3L_CNT;
-  p.lds3_MT = V3L_MT;
-  if (al(V3L_ENC_XE + SP * BS * 2) <= V3_LDS_2PERCU && Ld * p.in_stride * 4 <= V3_XDEC_BYTES) {
-    p.lds3_XDEC = V3L_XDEC;
-    p.lds3_ENC = V3L_ENC_XE;
-  } else {
-    p.lds3_XDEC = -1;
-    p.lds3_ENC = V3L_ENC;
-  }
-  p.lds3_bytes = al(p.lds3_ENC + SP * BS * 2);
+  if (max_cnt > LMAX * 96 || LP > LMAX || (c.enc_in & 3))
+    return fail(CET_E_INVALID, "fused LDS layout: multiplicity table or sequence length out of range");
   // v4: fixed regions (cet_plan.hpp v4_*) | stack output | [x_dec staged at entry, when two sequences
   // per CU still fit with it: its HBM latency then overlaps the LDS zeroing; else it is requested
   // before the last encoder norm, into CTX] | [sampler state: in-kernel replay path only]
@@ -803,7 +767,7 @@ int build_informer(cet_engine* e) {
     p.lds4_bytes = p.lds4_zero;
     p.lds4_xdec = -1;
     const int xdec_bytes = al(Ld * p.in_stride * 4);
-    if (p.lds4_bytes + xdec_bytes <= V3_LDS_2PERCU || P == 1) {
+    if (p.lds4_bytes + xdec_bytes <= V4_LDS_2PERCU || P == 1) {
       p.lds4_xdec = p.lds4_bytes;
       p.lds4_bytes += xdec_bytes;
     }
@@ -813,6 +777,25 @@ int build_informer(cet_engine* e) {
     p.lds4_bytes_replay = al(p.lds4_mt + MT_WORDS_HOST * 4);
     if (LMAX * p.in_stride * 4 > v4_ctx_bytes(P) || Ld > 48 || p.lds4_bytes_replay > 160 * 1024)
       return fail(CET_E_INVALID, "v4 LDS layout: staged input, decoder length or LDS size out of range");
+  }
+  // v5 (two sequences per workgroup, bf16 policy): the fixed per-sequence regions and the shared table
+  // (cet_plan.hpp v5_fixed), then per sequence the stack output, the staged x_dec and the labels, then
+  // the sampler state; v5_ok = 0 routes the plan to v4
+  {
+    const int RS = v4_rs(0);
+    p.lds5_enc = v5_fixed(0, V5_NS);
+    p.lds5_enc_stride = al(SP * RS);
+    p.lds5_zero = p.lds5_enc + V5_NS * p.lds5_enc_stride;
+    p.lds5_xdec = p.lds5_zero;
+    p.lds5_xdec_stride = al(Ld * p.in_stride * 4);
+    p.lds5_lab = p.lds5_xdec + V5_NS * p.lds5_xdec_stride;
+    p.lds5_lab_stride = al(c.out_len * c.c_out * 4);
+    p.lds5_bytes = p.lds5_lab + V5_NS * p.lds5_lab_stride;
+    p.lds5_mt = p.lds5_bytes;
+    p.lds5_bytes_replay = al(p.lds5_mt + MT_WORDS_HOST * 4);
+    // one f32x4 of x_enc / x_dec / labels per thread at kernel entry (512 threads)
+    p.v5_ok = P == 0 && p.lds5_bytes_replay <= 160 * 1024 && c.seq_len * c.enc_in <= 4 * 512 &&
+              Ld * c.dec_in <= 4 * 512 && c.out_len * c.c_out <= 4 * 512 && c.c_out <= 16;
   }
   p.stack = c.stack;
   return CET_OK;
@@ -1279,7 +1262,9 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   e->icfg = *cfg;
   e->generic = !fused_supported(*cfg) || std::getenv("CET_LAYERWISE") != nullptr;
   if (const char* v = std::getenv("CET_KERNEL"))
-    e->variant = std::strcmp(v, "v3") == 0 ? 3 : 4;
+    e->variant = std::strcmp(v, "v5") == 0 ? 5 : 4;
+  if (const char* v = std::getenv("CET_V5_MIN_B")) e->v5_min_b = std::max(1, std::atoi(v));
+  e->enc_split_ok = std::getenv("CET_NO_ENC_SPLIT") == nullptr;
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
   const auto& c = *cfg;
@@ -1451,40 +1436,44 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen) {
 
 static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   const InformerPlan& p = e->ip;
-  switch (e->variant) {
-    case 4: {
-      InformerArgs b = a;
-      b.wlo = (uint32_t)(e->wblob.size() * 2);
-      b.enc_split = 0;
-      b.enc_xchg = nullptr;
-      b.enc_count = nullptr;
-      // encoder split: the encoders of a stack are independent until the decoder, so at small batches
-      // each runs on its own workgroup (bf16 policy, no ProbSparse draws, production outputs only, the
-      // whole grid resident at two workgroups per CU)
-      static const bool no_split = std::getenv("CET_NO_ENC_SPLIT") != nullptr;
-      if (!no_split && e->prec == 0 && p.n_enc > 1 && p.n_calls == 0 && !a.attns && !a.dbg && !a.stamps &&
-          (int64_t)a.B * p.n_enc <= 512) {
-        const size_t words = (size_t)a.B * p.S * (v4_rs(0) / 8);
-        if (words > e->enc_xchg_n) {
-          if (e->d_enc_xchg) HIP_TRY(hipFree(e->d_enc_xchg));
-          HIP_TRY(hipMalloc((void**)&e->d_enc_xchg, words * sizeof(uint64_t)));
-          e->enc_xchg_n = words;
-        }
-        if (a.B > e->enc_count_n) {
-          if (e->d_enc_count) HIP_TRY(hipFree(e->d_enc_count));
-          HIP_TRY(hipMalloc((void**)&e->d_enc_count, (size_t)a.B * sizeof(unsigned)));
-          HIP_TRY(hipMemsetAsync(e->d_enc_count, 0, (size_t)a.B * sizeof(unsigned), st));   // re-armed by the kernel
-          e->enc_count_n = a.B;
-        }
-        b.enc_split = p.n_enc;
-        b.enc_xchg = e->d_enc_xchg;
-        b.enc_count = e->d_enc_count;
-      }
-      const bool replay = a.mt_in && !a.cnt;
-      return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);
-    }
-    default: return cet_launch_informer_v3(&a, e->icfg.d_ff, p.lds3_bytes, p.lds3_XDEC >= 0, st);
+  InformerArgs b = a;
+  b.wlo = (uint32_t)(e->wblob.size() * 2);
+  b.enc_split = 0;
+  b.enc_xchg = nullptr;
+  b.enc_count = nullptr;
+  const bool diag = a.attns || a.dbg || a.stamps;
+  const bool v4_only = a.attns != nullptr;   // attention maps: the v4 DIAG instance
+  const bool replay = a.mt_in && !a.cnt;
+  // encoder split (v4): the encoders of a stack are independent until the decoder, so at small batches
+  // each runs on its own workgroup (bf16 policy, no ProbSparse draws, production outputs only, the
+  // whole grid resident at two workgroups per CU)
+  const bool split = e->enc_split_ok && e->prec == 0 && p.n_enc > 1 && p.n_calls == 0 && !diag &&
+                     (int64_t)a.B * p.n_enc <= 512;
+  // v5: two sequences per workgroup (bf16 policy, production outputs, the plan fits its LDS layout)
+  if (e->variant == 5 && p.v5_ok && e->prec == 0 && !v4_only && !split && a.B >= e->v5_min_b) {
+    e->last_path = CET_PATH_V5;
+    return cet_launch_informer_v5(&b, e->prec, e->icfg.d_ff, replay ? p.lds5_bytes_replay : p.lds5_bytes, st);
   }
+  if (split) {
+    const size_t words = (size_t)a.B * p.S * (v4_rs(0) / 8);
+    if (words > e->enc_xchg_n) {
+      if (e->d_enc_xchg) HIP_TRY(hipFree(e->d_enc_xchg));
+      HIP_TRY(hipMalloc((void**)&e->d_enc_xchg, words * sizeof(uint64_t)));
+      e->enc_xchg_n = words;
+    }
+    if (a.B > e->enc_count_n) {
+      if (e->d_enc_count) HIP_TRY(hipFree(e->d_enc_count));
+      HIP_TRY(hipMalloc((void**)&e->d_enc_count, (size_t)a.B * sizeof(unsigned)));
+      e->enc_count_n = a.B;
+      // zeroed on every (re)allocation, on this launch's stream; the kernel re-arms it after each use
+      HIP_TRY(hipMemsetAsync(e->d_enc_count, 0, (size_t)a.B * sizeof(unsigned), st));
+    }
+    b.enc_split = p.n_enc;
+    b.enc_xchg = e->d_enc_xchg;
+    b.enc_count = e->d_enc_count;
+  }
+  e->last_path = split ? CET_PATH_V4_SPLIT : CET_PATH_V4;
+  return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);
 }
 
 static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, int B, float* out, float* attns,
@@ -1600,7 +1589,7 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
   a.nmse_sums = nullptr;
   // NMSE_Split of this forward's output: fused into the v4 kernel's epilogue (one n-tile of outputs),
   // else the standalone reduction right after the forward on the same stream
-  const bool fuse_nmse = label && e->variant == 4 && e->icfg.c_out <= 16;
+  const bool fuse_nmse = label && e->icfg.c_out <= 16;
   if (fuse_nmse) {
     const size_t need = (size_t)B * e->icfg.out_len;
     if (need > e->nmse_part_n) {
@@ -1630,7 +1619,7 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
   if (any_idx && !explicit_idx) return fail(CET_E_STATE, "ProbSparse indices set for some calls only");
   if (p.n_calls && !explicit_idx && !e->native_rng)
     return fail(CET_E_STATE, "ProbSparse indices not set (cet_set_prob_indices for every call, or cet_seed)");
-  if (e->variant >= 3 && e->native_rng && p.n_calls && !e->host_sampler && !explicit_idx) {
+  if (e->native_rng && p.n_calls && !e->host_sampler && !explicit_idx) {
     // ---- resident sampler: the kernel replays this forward's draws itself (cet_mt.hpp)
     if (!e->dev_mt_valid) {
       e->sync_host_rng();
@@ -1643,10 +1632,10 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
       e->dev_mt_valid = true;
       e->tab_ready = false;
     }
-    const bool prep = e->variant >= 3 && B >= cet_engine::PREP_MIN_B;
+    const bool prep = B >= cet_engine::PREP_MIN_B;
     if (prep && !e->tab_ready) {
       // first forward after a (re)seed: this forward's tables from a one-workgroup launch
-      const int lds = std::max(640 * 4 + (p.lds3_MT - p.lds3_CNT), std::min(replay_fast_lds(p), 64 * 1024));
+      const int lds = std::max(640 * 4 + LMAX * 96, std::min(replay_fast_lds(p), 64 * 1024));
       if (cet_launch_sampler_prep((const InformerPlan*)e->d_plan, e->d_mt + 640 * e->mt_cur,
                                   e->d_mt + 640 * (1 - e->mt_cur), e->d_tab[e->tab_cur], lds, st))
         return fail(CET_E_HIP, std::string("sampler prep launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1689,7 +1678,6 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
   e->slot = (e->slot + 1) % cet_engine::NSLOT;
   if (e->ev_used[k]) HIP_TRY(hipEventSynchronize(e->ev[k]));
   uint8_t* h = e->h_cnt[k];
-  const bool v2 = e->variant >= 3;   // v3 count-row layout (cnt_pos_v2)
   if (p.n_calls) {
     std::memset(h, 0, e->cnt_bytes);
     for (int c = 0; c < p.n_calls; ++c) {
@@ -1700,14 +1688,14 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
         for (int q = 0; q < sh.LQ; ++q)
           for (int j = 0; j < sh.U; ++j) {
             const int key = (int)(e->rng.next() % (uint32_t)sh.LK);
-            tab[q * ac.cnt_stride + (v2 ? cnt_pos_v2(key) : key)]++;
+            tab[q * ac.cnt_stride + cnt_pos_v2(key)]++;
           }
       } else {
         const int32_t* id = e->idx[c].data();
         for (int q = 0; q < sh.LQ; ++q)
           for (int j = 0; j < sh.U; ++j) {
             const int key = id[q * sh.U + j];
-            tab[q * ac.cnt_stride + (v2 ? cnt_pos_v2(key) : key)]++;
+            tab[q * ac.cnt_stride + cnt_pos_v2(key)]++;
           }
       }
     }
@@ -1758,12 +1746,16 @@ int cet_set_sampler(cet_engine* e, int on_host) {
 
 int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
-  if (variant != 3 && variant != 4)
-    return fail(CET_E_INVALID, "variant must be 3 or 4 (the round-1 LDS-resident kernel 1 is retired)");
-  if (variant != e->variant) e->dirty = true;   // the precision resolution depends on the kernel
+  if (variant != 4 && variant != 5)
+    return fail(CET_E_INVALID, "variant must be 4 (one sequence per workgroup) or 5 (two); 1-3 are retired");
   if (e->kind != 0 && variant != 4) return fail(CET_E_INVALID, "the Transformer engine has variant 4 only");
   e->variant = variant;
   return CET_OK;
+}
+
+int cet_last_path(cet_engine* e) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  return e->last_path;
 }
 
 int cet_timing(cet_engine* e, int enable) {

@@ -15,38 +15,6 @@
 namespace cet {
 namespace v4 {
 
-template <int N>
-using IC = std::integral_constant<int, N>;
-
-__device__ __forceinline__ void stage(const float* __restrict__ src, float* dst, int L, int C, int CS) {
-  for (int i = threadIdx.x; i < L * C; i += NTHREADS) {
-    const int t = i / C, c = i - t * C;
-    dst[t * CS + c] = src[i];
-  }
-}
-
-// Plan access point: read through the constant address space behind an opaque pointer, so each
-// phase re-loads its descriptors with scalar loads instead of keeping them live in SGPRs.
-#if defined(__HIP_DEVICE_COMPILE__)
-template <class T>
-using cptr = const __attribute__((address_space(4))) T*;
-#else
-template <class T>
-using cptr = const T*;
-#endif
-template <class T>
-__device__ __forceinline__ cptr<T> fresh(const T* p) {
-  cptr<T> c = (cptr<T>)p;
-  asm volatile("" : "+s"(c));
-  return c;
-}
-
-__device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
-  if (d.bias != NONE) d.bias += off;
-  if (d.scale != NONE) d.scale += off;
-  return d;
-}
-
 // P: precision of the dense (LSQ-quantisable) layers; DIAG: the instance that honours the optional
 // outputs (attns maps, activation dumps, phase stamps) — the production instance compiles them out.
 template <int DFF, bool DIAG, int P, bool SPLIT = false>
@@ -300,8 +268,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     __syncthreads();
     unsigned* tk = reinterpret_cast<unsigned*>(lds + v4_scr(P));
     if (threadIdx.x == 0) {
-      const unsigned t = atomicAdd(a.enc_count + b, 1u);
-      if (t + 1u == (unsigned)nsplit) atomicExch(a.enc_count + b, 0u);   // re-arm for the next launch
+      // agent-scope acq_rel arrival: the rows published above are ordered before the count, and the
+      // last arrival's reads of the other workgroups' rows after it (not only by the sc1 codegen)
+      const unsigned t = __hip_atomic_fetch_add(a.enc_count + b, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == (unsigned)nsplit)   // re-arm for the next launch
+        __hip_atomic_store(a.enc_count + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *tk = t;
     }
     __syncthreads();
@@ -458,8 +429,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     __syncthreads();   // every wave's NMSE partials are written (each waited for its own stores)
     unsigned* tk = reinterpret_cast<unsigned*>(lds + v4_scr(P));
     if (threadIdx.x == 0) {
-      const unsigned t = atomicAdd(a.ticket, 1u);   // agent-scope add, value returned
-      if (t + 1u == (unsigned)a.B) atomicExch(a.ticket, 0u);   // re-arm for the next launch
+      // agent-scope acq_rel arrival: this workgroup's NMSE partials are ordered before the count, and
+      // the last arrival's reads of every partial after it
+      const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1u == (unsigned)a.B)   // re-arm for the next launch
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *tk = t;
     }
     __syncthreads();   // the other waves load after this barrier (the adding wave has its value)

@@ -16,8 +16,8 @@ struct InformerArgs {
   const uint8_t* cnt;         // per-forward ProbSparse key multiplicities (host-built), or
   const uint32_t* mt_in;      // resident mt19937 state slot to replay the draws from, and
   uint32_t* mt_out;           //     the slot workgroup 0 writes the advanced state to
-  uint8_t* cnt_next;          // v3: where the first workgroup to finish writes the next forward's tables
-  unsigned* ticket;           // v3: finish counter for that election (the last finisher re-arms it)
+  uint8_t* cnt_next;          // where the first workgroup to finish writes the next forward's tables
+  unsigned* ticket;           // finish counter for that election (the last finisher re-arms it)
   const float* x_enc;         // [B][seq_len][C]
   const float* x_dec;         // [B][dec_len][C]
   float* out;                 // [B][pred_len][c_out]
@@ -86,9 +86,8 @@ bool ensure_lds_attr(const void* kern);
 
 extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
                                        uint8_t* tab_out, int lds_bytes, hipStream_t stream);
-extern "C" int cet_launch_informer_v3(const cet::InformerArgs* a, int dff, int lds_bytes, int xdec_early,
-                                      hipStream_t stream);
 extern "C" int cet_launch_informer_v4(const cet::InformerArgs* a, int prec, int dff, int lds_bytes, hipStream_t stream);
+extern "C" int cet_launch_informer_v5(const cet::InformerArgs* a, int prec, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);

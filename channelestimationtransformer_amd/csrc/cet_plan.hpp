@@ -24,7 +24,7 @@ __host__ __device__ inline int cnt_word_off(int key) { return ((key >> 2) & 3) *
 __host__ __device__ inline int cnt_pos_v2(int key) { return cnt_word_off(key) + (key & 3); }
 // v2 per-wave attention scratch: 96 u64 selection keys | 96 int16 selected rows | 96 flag bytes
 constexpr int V2_SCR_FLOATS = 264;
-// v3 LayerNorm partials: floats per row (8 waves × (mean, M2) + pad; 80-byte rows put 16
+// LayerNorm partials: floats per row (8 waves × (mean, M2) + pad; 80-byte rows put 16
 // consecutive rows on distinct bank quads)
 constexpr int LN3_STRIDE = 20;
 
@@ -86,19 +86,16 @@ struct InformerPlan {
   AttnCall calls[MAX_CALLS];
   int n_calls;
   uint32_t cnt_bytes;
-  // LDS layout (byte offsets) and size
-  int lds_X, lds_Q, lds_K, lds_VT, lds_ENC, lds_CTX, lds_M, lds_SEL, lds_FLAG, lds_bytes;
-  int vts;
-  // v2 (register-resident) kernel LDS layout
-  int lds2_XB, lds2_CTX, lds2_ENC, lds2_LN, lds2_SCR, lds2_CNT, lds2_MT, lds2_bytes;
-  // v3 (8-wave) layout: the LayerNorm partials alias the per-wave attention scratch
-  int lds3_XB, lds3_CTX, lds3_ENC, lds3_SCR, lds3_CNT, lds3_MT, lds3_bytes;
-  int lds3_XDEC;            // staged decoder input (byte offset), or -1
   // v4 layout (cet_plan.hpp v4_*): the fixed regions, the encoder-stack output (planes × S_pad rows),
   // the staged x_dec and, for the in-kernel sampler replay, its state
   int lds4_enc, lds4_enc_lo, lds4_cnt, lds4_mt, lds4_zero, lds4_bytes, lds4_bytes_replay;
   int lds4_xdec;            // x_dec staged at kernel entry (byte offset), or -1: staged before the decoder
   int lds4_lab;             // labels of the fused NMSE (pred_len × c_out fp32), staged at kernel entry
+  // v5 layout (cet_v5.hpp L5: NS sequences per workgroup): after the fixed per-sequence regions and
+  // the shared multiplicity table, per sequence the stack output, the staged x_dec and the labels, then
+  // the sampler state (in-kernel replay only); v5_ok = 0 when the plan does not fit (v4 runs it)
+  int lds5_enc, lds5_enc_stride, lds5_xdec, lds5_xdec_stride, lds5_lab, lds5_lab_stride;
+  int lds5_zero, lds5_mt, lds5_bytes, lds5_bytes_replay, v5_ok;
   int prec;                 // v4 operand precision of the dense layers (v4::P_BF16 / P_X3 / P_FP8)
   int stack;
   int in_stride;            // floats per staged input row
@@ -106,33 +103,12 @@ struct InformerPlan {
   int draws;                // mt19937 words one forward consumes (Σ LQ·U over every call)
 };
 
-// v3 LDS layout, fixed at compile time for every plan (LMAX rows; the kernel folds the offsets into
-// its ds_* immediates and keeps no LDS base in scalar registers): bf16 image | context / FFN hidden /
-// staged input | 8 waves' attention scratch aliased by the LayerNorm partials | multiplicity table |
-// sampler state | [staged decoder input] | encoder-stack output (S rows, the only plan-sized
-// region, last).
-constexpr int V3L_XB = 0;
-constexpr int V3L_CTX = V3L_XB + LMAX * BS * 2;
-constexpr int V3L_SCR = V3L_CTX + LMAX * BS * 2;
-constexpr int V3L_CNT = V3L_SCR + (LMAX * LN3_STRIDE * 4 > 8 * V2_SCR_FLOATS * 4 ? LMAX * LN3_STRIDE * 4
-                                                                                 : 8 * V2_SCR_FLOATS * 4);
-constexpr int V3L_MT = V3L_CNT + LMAX * 96;
-constexpr int V3L_XDEC = V3L_MT + ((624 * 4 + 15) & ~15);   // staged decoder input, ≤ 48 rows × 20
-constexpr int V3_XDEC_BYTES = 48 * 20 * 4;
-constexpr int V3L_ENC_XE = V3L_XDEC + V3_XDEC_BYTES;   // stack output after the staged decoder input
-constexpr int V3L_ENC = V3L_XDEC;                      // ... or in its place (decoder input staged late)
-constexpr int V3_LDS_2PERCU = 80 * 1024;               // two sequences per CU
-// The kernel instance with the x_dec region (XE) is used when the plan still fits two workgroups
-// per CU with it (InformerPlan::lds3_XDEC = V3L_XDEC), else x_dec is staged into CTX when the
-// decoder starts (lds3_XDEC = -1).
-static_assert(V3L_CTX % 16 == 0 && V3L_SCR % 16 == 0 && V3L_CNT % 16 == 0 && V3L_ENC_XE % 16 == 0, "16-B regions");
-
 // v4 LDS layout (precision P: 0 bf16, 1 split-bf16 hi/lo planes, 2 fp8); every offset the kernel
 // uses in its phases is a compile-time constant (folded into ds_* immediates):
 //   image XB | context / FFN hidden / staged input / projection input (CTX) | per-wave attention
 //   scratch aliased by the LayerNorm partials | multiplicity table | stack output (plan-sized) |
 //   [x_dec staged at entry] | [sampler state, in-kernel replay only]
-// Image rows: bf16 272 B (v3's stride; 288 B — conflict-free ds_read_b128 — measured no faster), fp8
+// Image rows: bf16 272 B ( 288 B — conflict-free ds_read_b128 — measured no faster), fp8
 // 144 B (conflict-free ds_read_b64).
 #ifndef V4_RS16
 #define V4_RS16 272   // A/B knob: bf16 image row stride (bytes); 288 (conflict-free ds_read_b128) measured equal
@@ -142,6 +118,7 @@ constexpr int v4_planes(int P) { return P == 1 ? 2 : 1; }
 constexpr int v4_img(int P) { return LMAX * v4_rs(P); }
 constexpr int v4_max3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
 constexpr int V4L_XB = 0;
+constexpr int V4_LDS_2PERCU = 80 * 1024;   // two workgroups per CU
 constexpr int v4_ctx(int P) { return v4_planes(P) * v4_img(P); }
 constexpr int v4_ctx_bytes(int P) {
   // context image | staged fp32 input rows (LMAX × 20 floats) | the bf16 projection input (48 rows)
@@ -153,6 +130,12 @@ constexpr int v4_enc(int P) { return v4_cnt(P) + LMAX * 96; }               // s
 static_assert(LMAX * LN3_STRIDE * 4 + LMAX * 8 <= 8 * V2_SCR_FLOATS * 4,
               "LN partials and row statistics fit the scratch they alias");
 static_assert(v4_ctx(0) % 16 == 0 && v4_scr(0) % 16 == 0 && v4_enc(1) % 16 == 0 && v4_enc(2) % 16 == 0, "16-B");
+
+// v5 layout (cet_v5.hpp L5): per sequence image | context | attention scratch, NS times; then the
+// multiplicity table shared by the sequences; then the plan-sized regions (InformerPlan::lds5_*).
+constexpr int V5_NS = 2;   // sequences per workgroup
+constexpr int v5_seq(int P) { return v4_img(P) + v4_ctx_bytes(P) + 8 * V2_SCR_FLOATS * 4; }
+constexpr int v5_fixed(int P, int ns) { return ns * v5_seq(P) + LMAX * 96; }
 
 // LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded
 // mt19937 state | the forward's tempered words | every call's multiplicity table.

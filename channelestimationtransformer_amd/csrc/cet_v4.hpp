@@ -684,6 +684,38 @@ __device__ __forceinline__ void maxpool_eo(const Res<NIN>& in, int L, Res<MT>& o
   for (int j = NOUT; j < MT; ++j) out.v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+template <int N>
+using IC = std::integral_constant<int, N>;
+
+__device__ __forceinline__ void stage(const float* __restrict__ src, float* dst, int L, int C, int CS) {
+  for (int i = threadIdx.x; i < L * C; i += NTHREADS) {
+    const int t = i / C, c = i - t * C;
+    dst[t * CS + c] = src[i];
+  }
+}
+
+// Plan access point: read through the constant address space behind an opaque pointer, so each
+// phase re-loads its descriptors with scalar loads instead of keeping them live in SGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
+#else
+template <class T>
+using cptr = const T*;
+#endif
+template <class T>
+__device__ __forceinline__ cptr<T> fresh(const T* p) {
+  cptr<T> c = (cptr<T>)p;
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
+__device__ __forceinline__ GemmDesc part_of(GemmDesc d, int off) {
+  if (d.bias != NONE) d.bias += off;
+  if (d.scale != NONE) d.scale += off;
+  return d;
+}
+
 // ------------------------------------------------------------------------------ attention
 // One head per wave, everything in registers: Kᵀ = Wk_h·Xᵀ (A of Sᵀ = K·Qᵀ), Qᵀ = Wq_h·Xᵀ (B of Sᵀ),
 // V = X·Wv_hᵀ (A of Oᵀ = Vᵀ·Pᵀ), and the exponentiated Sᵀ tile is the B fragment of Oᵀ.

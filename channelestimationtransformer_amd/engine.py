@@ -133,6 +133,38 @@ class Engine:
         check(lib.cet_forward_nmse(self._h, ptr(x_enc), ptr(x_dec), B, ptr(out), ptr(label), ptr(nmse_acc),
                                    ptr(nmse_sums), ctypes.c_void_p(stream)), "cet_forward_nmse")
 
+    def bind_forward_nmse(self, x_enc, x_dec, out, label, nmse_sums, stream: Optional[int] = None):
+        """A step function for a loop over fixed device buffers: ``step(k)`` runs ``forward_nmse`` with the
+        raw sums going to ``nmse_sums[k]`` (float64 [steps, 2, T]), the argument checks and pointer
+        conversions done once here instead of per step (the host cost of a step stays far below the
+        kernel's even on a loaded host)."""
+        import torch
+
+        B, T = int(x_enc.shape[0]), int(out.shape[1])
+        if tuple(label.shape) != tuple(out.shape) or label.dtype != torch.float32 or not label.is_contiguous():
+            raise ValueError("label must be a contiguous float32 tensor shaped like out")
+        if nmse_sums.dtype != torch.float64 or not nmse_sums.is_contiguous() or tuple(nmse_sums.shape[1:]) != (2, T):
+            raise ValueError(f"nmse_sums must be a contiguous float64 [steps, 2, {T}]")
+        for t in (x_enc, x_dec, out):
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("x_enc, x_dec and out must be contiguous float32")
+        if stream is None:
+            stream = _stream_ptr(x_enc.device)
+        f, h = lib.cet_forward_nmse, self._h
+        args = [ctypes.c_void_p(t.data_ptr()) for t in (x_enc, x_dec)] + [B] + \
+               [ctypes.c_void_p(t.data_ptr()) for t in (out, label)] + [None]
+        s0, stride, n = nmse_sums.data_ptr(), 2 * T * 8, int(nmse_sums.shape[0])
+        st = ctypes.c_void_p(stream)
+
+        def step(k: int) -> None:
+            if not 0 <= k < n:
+                raise IndexError(k)
+            rc = f(h, *args, s0 + k * stride, st)
+            if rc < 0:
+                check(rc, "cet_forward_nmse")
+
+        return step
+
     def attns_floats(self) -> int:
         return check(lib.cet_attns_floats(self._h), "cet_attns_floats")
 
@@ -152,8 +184,16 @@ class Engine:
         check(lib.cet_set_sampler(self._h, int(bool(on_host))), "cet_set_sampler")
 
     def set_variant(self, variant: int) -> None:
-        """Fused-kernel generation: 4 (default) or 3 (its bf16-only predecessor)."""
+        """Fused-kernel generation: 4 (default: one sequence per workgroup; every precision policy and the
+        diagnostic outputs) or 5 (two sequences per workgroup where the plan allows, bit-for-bit v4's
+        outputs)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
+
+    PATHS = {0: None, 4: "v4", 5: "v5", 41: "v4-split"}
+
+    def last_path(self):
+        """The fused kernel the last Informer forward launched: "v5", "v4", "v4-split" or None."""
+        return self.PATHS[check(lib.cet_last_path(self._h), "cet_last_path")]
 
     PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3}
 

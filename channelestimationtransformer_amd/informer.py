@@ -148,6 +148,15 @@ class _EngineModule(nn.Module):
         """Force re-packing of the weights at the next forward."""
         self._synced_version = None
 
+    def _apply(self, fn, *args, **kwargs):
+        # .to() / .cuda() / .double() / .half() replace parameters and buffers by writing
+        # self._parameters / self._buffers directly, which fires no registration hook: forget the tracked
+        # tensor set so the next staleness check re-walks the state_dict and watches the new tensors
+        self._tensors_at = None
+        self._tensors = None
+        self._synced_version = None
+        return super()._apply(fn, *args, **kwargs)
+
     def train(self, mode: bool = True):
         return super().train(mode)
 

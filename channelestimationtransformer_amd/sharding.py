@@ -10,9 +10,11 @@ shards with no data-path collective.  The only exchanges happen after the timed 
   per-batch ratios (``QuantizationAwareTraining.py:122,138``);
 * ``gather_predictions``: the north star's RCCL all-gather — rank 0 collates the last step's
   predictions (and labels) of every rank and reduces NMSE_Split over them itself, which must agree
-  with the all-reduced sums of that step (``check_gathered_nmse``);
-* ``collate_nmse``: the SNR sweep's variant, where every rank holds whole reference batches and the
-  per-batch ratios are summed.
+  with the all-reduced sums of that step (``check_gathered_nmse``).
+
+bench.py and the SNR sweep (``sweep.run_snr_point``) both collate this way.  A reference batch of the
+multi-GPU sweep is the N ranks' shards of one step (C4: 8 × 512 = 4096 sequences per batch), so its
+NMSE is NMSE_Split over the whole global batch, as the reference computes it over one 4096 batch.
 
 Works with any torch.distributed backend: ``nccl`` (RCCL over xGMI) on the GPU node, ``gloo``
 in the CPU tests.
@@ -27,15 +29,6 @@ def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     base, extra = divmod(total, world)
     start = rank * base + min(rank, extra)
     return start, start + base + (1 if rank < extra else 0)
-
-
-def collate_nmse(acc, n_batches_per_rank: int, world: int, group=None):
-    """Global mean of per-batch NMSE ratios from per-rank sums (all_reduce, SUM)."""
-    import torch.distributed as dist
-
-    if world > 1:
-        dist.all_reduce(acc, group=group)
-    return acc / float(n_batches_per_rank * world)
 
 
 def collate_step_sums(sums, world: int, group=None):

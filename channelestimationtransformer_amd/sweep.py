@@ -67,14 +67,54 @@ def load_dataset(path):
     return obj
 
 
+def run_snr_point(step, n_batches, T, world=1, rank=0, dist=None, nmse_fn=None, device=None, synchronize=None):
+    """One SNR of the sweep, with the engine abstracted away (so the collation runs on CPU under gloo too).
+
+    ``step(i, sums_row)`` runs reference batch i of this rank (its shard of ``world`` shards) and writes
+    that shard's raw NMSE_Split sums (float64 [2, T]: Σ(x − x̂)², Σx̂²) into ``sums_row``; it returns the
+    shard's (predictions, labels).  After the loop one all_reduce gives every batch's ratio over the
+    whole global batch (``NMSE_Split_cuda`` over all N × batch predictions), their mean is
+    ``run_validation``'s ``loss / len(loader)`` (QuantizationAwareTraining.py:122,138), and rank 0
+    checks NMSE_Split over the all-gathered last predictions (``nmse_fn``) against the all-reduced sums.
+    Returns {nmse [T] numpy, ratios [n_batches, T] numpy, seconds (max over ranks), check}."""
+    import torch
+
+    from .sharding import check_gathered_nmse, collate_step_sums, gather_predictions
+
+    sync = synchronize or (lambda: None)
+    sums = torch.zeros(n_batches, 2, T, dtype=torch.float64, device=device)
+    sync()
+    t0 = time.perf_counter()
+    out = lab = None
+    for i in range(n_batches):
+        out, lab = step(i, sums[i])
+    sync()
+    dt = time.perf_counter() - t0
+    if dist is not None and world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ratios, nmse = collate_step_sums(sums, world)
+    preds, labels = gather_predictions(out, world), gather_predictions(lab, world)
+    check = None
+    if rank == 0 and nmse_fn is not None:
+        g = nmse_fn(torch.cat(preds).contiguous(), torch.cat(labels).contiguous())
+        check = check_gathered_nmse(g, ratios[-1])
+    return {"nmse": nmse.cpu().numpy(), "ratios": ratios.cpu().numpy(), "seconds": dt, "check": check}
+
+
 def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=None, seed=0, rank=0, world=1,
-              device=None, dist=None):
-    """Yields one result dict per SNR (identical on every rank)."""
+              device=None, dist=None, capture=None):
+    """Yields one result dict per SNR (identical on every rank).
+
+    ``capture(snr, i, x_enc, x_dec, out, label)``, if given, sees every batch this rank ran (device
+    tensors, valid until the next batch): the tests check the sweep's NMSE and predictions against the
+    oracle with it.  The ProbSparse draws are the native stream seeded with ``1 + seed``, one forward's
+    worth per batch in order."""
     import torch
 
     from .engine import nmse_split
     from .pipeline import DeviceSeqData, synth_channels
-    from .sharding import check_gathered_nmse, collate_step_sums, gather_predictions
 
     c = CONFIG
     model = build_model(device, checkpoint)
@@ -97,32 +137,25 @@ def run_sweep(snrs, batch, batches, dataset=None, n_samples=None, checkpoint=Non
     for k, snr in enumerate(snrs):
         g = torch.Generator().manual_seed(seed * 1000 + k)
         perm = torch.randperm(len(data), generator=g).to(torch.int32).to(device)   # the loader's shuffle
-        sums = torch.zeros(n_batches, 2, c["pred_len"], dtype=torch.float64, device=device)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for i in range(n_batches):
+
+        def step(i, sums_row):
             off = (i * world + rank) * batch
             xe, xd, lb = data.batch(idx=perm[off:off + batch], seed=seed, counter=(k << 32) + i * world + rank,
                                     snr=snr, out=bufs, stream=stream)
-            eng.forward_nmse(xe, xd, out, lb, None, sums[i], stream)   # forward + NMSE_Split, one launch
-        torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
-        if dist is not None:
-            t = torch.tensor([dt], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        ratios, nmse = collate_step_sums(sums, world)
-        preds, labels = gather_predictions(out, world), gather_predictions(bufs[2], world)
-        check = None
-        if rank == 0:
-            g = nmse_split(torch.cat(preds).contiguous(), torch.cat(labels).contiguous())
-            check = check_gathered_nmse(g, ratios[-1])
-        nmse = nmse.cpu().numpy()
+            eng.forward_nmse(xe, xd, out, lb, None, sums_row, stream)   # forward + NMSE_Split, one launch
+            if capture is not None:
+                capture(snr, i, xe, xd, out, lb)
+            return out, lb
+
+        r = run_snr_point(step, n_batches, c["pred_len"], world, rank, dist, lambda p, y: nmse_split(p, y), device,
+                          lambda: torch.cuda.synchronize(device))
+        nmse = r["nmse"]
         seqs = n_batches * batch * world
         yield {"snr": snr, "nmse": [float(v) for v in nmse], "nmse_db": [round(float(10 * np.log10(v)), 4) for v in nmse],
                "nmse_db_mean": round(float(10 * np.log10(nmse.mean())), 4), "batches": n_batches,
-               "global_batch": batch * world, "sequences": seqs, "seconds": round(dt, 4),
-               "seq_per_s": round(seqs / dt, 1), "world": world, "nmse_gathered_vs_allreduced_rel": check}
+               "global_batch": batch * world, "sequences": seqs, "seconds": round(r["seconds"], 4),
+               "seq_per_s": round(seqs / r["seconds"], 1), "world": world,
+               "nmse_gathered_vs_allreduced_rel": r["check"], "kernel_path": eng.last_path()}
 
 
 def main(argv=None):

@@ -4,7 +4,9 @@
  * sizes only; device pointers are HIP device memory, `stream` is a hipStream_t
  * (NULL = default stream).  Every function returns 0 on success and a negative code
  * on error; cet_last_error() then describes it (thread-local).  A handle is not
- * thread-safe; use one handle per host thread / stream.
+ * thread-safe, and its forwards must not overlap on different streams: the engine's device scratch
+ * (table ring, NMSE partials and finish counter, encoder-split exchange) is per handle.  Use one
+ * handle per host thread / stream.
  *
  * Reference interfaces each entry point replaces (paths relative to the reference repo):
  *   cet_create_informer      InformerStack.__init__ / Informer.__init__
@@ -116,11 +118,19 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen);
 /* Diagnostics (DIAG kernel instance): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
 
-/* Select the fused-kernel generation of an Informer engine: 4 (default: 8-wave register-resident,
- * two sequences per CU, precision policies) or 3 (its bf16-only predecessor).  CET_KERNEL=v3 in the
- * environment selects 3 at creation.  Transformer engines have generation 4 only.  (Generation 1, the
- * round-1 LDS-resident kernel, is retired: CET_E_INVALID.) */
+/* Select the fused-kernel generation of an Informer engine: 4 (default: one sequence per 512-thread
+ * workgroup, two workgroups per CU, every precision policy, the attention maps and the small-batch
+ * encoder split) or 5 (TWO sequences per workgroup, one workgroup per CU, 256 VGPRs, every weight
+ * fragment shared by both sequences; bf16 policy, production outputs, activation dumps and phase
+ * stamps — other cases run generation 4; the same arithmetic per sequence, outputs bit-for-bit equal to
+ * generation 4's).  CET_KERNEL=v5 in the environment selects 5 at creation; CET_V5_MIN_B=n sends
+ * batches below n to generation 4.  Transformer engines have generation 4 only.  Generations 1-3 are
+ * retired: CET_E_INVALID. */
 int cet_set_variant(cet_engine* e, int variant);
+/* The fused kernel the engine's last Informer forward launched: CET_PATH_V5, CET_PATH_V4,
+ * CET_PATH_V4_SPLIT (v4 with the stack's encoders on separate workgroups), 0 before any. */
+enum { CET_PATH_V4 = 4, CET_PATH_V5 = 5, CET_PATH_V4_SPLIT = 41 };
+int cet_last_path(cet_engine* e);
 
 /* Operand precision of the v4 kernel's dense layers (Informer engines):
  *   -1 auto (default): 0, or 1 where bf16 cannot carry the model — an LSQ integer grid with |q| > 256,
@@ -140,7 +150,7 @@ int cet_set_variant(cet_engine* e, int variant);
 int cet_set_precision(cet_engine* e, int prec);
 int cet_get_precision(cet_engine* e);
 
-/* Where the native sampler (after cet_seed) runs for variant 3: 0 = on the device (the
+/* Where the native sampler (after cet_seed) runs: 0 = on the device (the
  * resident mt19937, default), 1 = on the host (the same torch-compatible stream drawn by the host
  * mirror, the multiplicity tables staged per forward through a pinned ring and copied on the
  * caller's stream ahead of the kernel).  Both give identical draws; switching keeps the stream.

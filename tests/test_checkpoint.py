@@ -111,3 +111,25 @@ def test_weight_staleness_check_is_cheap_and_complete():
     assert v5 != v4
     torch.nn.Linear(3, 3)   # another module's registrations do not invalidate this one
     assert m._version() == v5
+
+
+def test_staleness_survives_module_apply():
+    """Module._apply (.double() / .float() / .to()) swaps parameters and buffers without registration
+    hooks: the check must watch the new tensors, so a later in-place edit of a buffer (the positional
+    table, BatchNorm running stats) is still seen."""
+    m = _model().eval()
+    v0 = m._version()
+    m.double()
+    v1 = m._version()
+    assert v1 != v0
+    pe = m.enc_embedding.position_embedding.pe
+    assert pe.dtype == torch.float64
+    with torch.no_grad():
+        pe.add_(1.0)
+    v2 = m._version()
+    assert v2 != v1
+    m.float()
+    v3 = m._version()
+    with torch.no_grad():
+        dict(m.named_buffers())["encoder.encoders.0.conv_layers.0.norm.running_var"].mul_(2.0)
+    assert m._version() != v3

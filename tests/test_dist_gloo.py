@@ -2,7 +2,8 @@
 
 Each rank predicts its contiguous shard (the CPU oracle stands in for the GPU engine here),
 accumulates NMSE_Split, then the collectives of :mod:`channelestimationtransformer_amd.sharding`
-must reproduce the unsharded computation exactly.
+— driven through the SNR sweep's own per-SNR loop, ``sweep.run_snr_point`` — must reproduce the
+unsharded computation.
 """
 import os
 import socket
@@ -12,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from channelestimationtransformer_amd.sharding import collate_nmse, gather_predictions, shard_range
+from channelestimationtransformer_amd.sharding import shard_range
 
 
 def _free_port():
@@ -23,6 +24,9 @@ def _free_port():
     return p
 
 
+PER_RANK, N_BATCHES = 3, 2   # a global reference batch = world × PER_RANK sequences (C4: 8 × 512)
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -31,24 +35,25 @@ def _worker(rank, world, port, q):
 
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from channelestimationtransformer_amd.dataset import make_batch
+        from channelestimationtransformer_amd.sharding import nmse_split_torch
+        from channelestimationtransformer_amd.sweep import run_snr_point
         from golden_util import load_case, oracle_for
-        from oracle.metrics_np import nmse_split
 
         case = load_case("informer_prob_b4")
         orc = oracle_for(case)
-        total, per_batch = 8, 2
-        xe, xd, lab = make_batch(total, seed=3)
-        lo, hi = shard_range(total, world, rank)
-        acc = torch.zeros(5, dtype=torch.float64)
-        preds = []
-        for b0 in range(lo, hi, per_batch):   # whole reference batches per rank
-            out, _ = orc.forward(xe[b0:b0 + per_batch], xd[b0:b0 + per_batch], case.idx)
-            preds.append(out)
-            acc += torch.from_numpy(nmse_split(out, lab[b0:b0 + per_batch]))
-        nmse = collate_nmse(acc, (hi - lo) // per_batch, world)
-        gathered = gather_predictions(torch.from_numpy(np.concatenate(preds)), world)
+        xe, xd, lab = make_batch(world * PER_RANK * N_BATCHES, seed=3)
+
+        def step(i, sums_row):   # this rank's shard of global batch i (sweep.run_sweep's indexing)
+            off = (i * world + rank) * PER_RANK
+            out, _ = orc.forward(xe[off:off + PER_RANK], xd[off:off + PER_RANK], case.idx)
+            p, y = torch.from_numpy(out), torch.from_numpy(lab[off:off + PER_RANK])
+            d = y.double() - p.double()
+            sums_row[0], sums_row[1] = (d * d).sum((0, 2)), (p.double() ** 2).sum((0, 2))
+            return p.float(), y
+
+        r = run_snr_point(step, N_BATCHES, 5, world, rank, dist, nmse_split_torch)
         if rank == 0:
-            q.put((nmse.numpy(), torch.cat(gathered).numpy()))
+            q.put((r["nmse"], r["ratios"], r["check"]))
     finally:
         dist.destroy_process_group()
 
@@ -63,7 +68,11 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
 
 
-def test_two_rank_collation_matches_unsharded():
+def test_two_rank_sweep_collation_matches_unsharded():
+    """The SNR sweep's per-SNR loop and collation (sweep.run_snr_point: per-rank raw sums, all_reduce,
+    all_gather of the last predictions, rank 0's check) at world 2 over gloo: every global batch's
+    ratio equals NMSE_Split over that batch's unsharded predictions, and the reported NMSE is their
+    mean (run_validation's mean of per-batch ratios)."""
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -77,18 +86,21 @@ def test_two_rank_collation_matches_unsharded():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    nmse, preds = q.get(timeout=300)
+    nmse, ratios, check = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
 
     case = load_case("informer_prob_b4")
     orc = oracle_for(case)
-    xe, xd, lab = make_batch(8, seed=3)
+    G = 2 * PER_RANK
+    xe, xd, lab = make_batch(G * N_BATCHES, seed=3)
     ref_preds, _ = orc.forward(xe, xd, case.idx)
-    np.testing.assert_allclose(preds, ref_preds, rtol=1e-12, atol=1e-12)
-    ref = np.mean([nmse_split(ref_preds[b:b + 2], lab[b:b + 2]) for b in range(0, 8, 2)], axis=0)
-    np.testing.assert_allclose(nmse, ref, rtol=1e-12)
+    ref = np.stack([nmse_split(ref_preds[i * G:(i + 1) * G].astype(np.float32), lab[i * G:(i + 1) * G])
+                    for i in range(N_BATCHES)])
+    np.testing.assert_allclose(ratios, ref, rtol=1e-6)
+    np.testing.assert_allclose(nmse, ref.mean(0), rtol=1e-6)
+    assert check is not None and check < 1e-5
 
 
 def test_bench_spawns_its_ranks_and_collates_by_gather():

@@ -41,6 +41,9 @@ def main():
     torch.cuda.synchronize()
     eng.set_stamps(None)
     s = st.view(B, 128).cpu().numpy().astype(np.int64)
+    rows = s[:, 0] != 0        # v5 stamps each workgroup (two sequences) in its first sequence's row
+    s = s[rows]
+    print(f"kernel path: {eng.last_path()}  stamped workgroups: {int(rows.sum())}")
     n = len(NAMES)
     s = s[:, :n]
     d = np.diff(s, axis=1)
@@ -49,7 +52,7 @@ def main():
     start = s[:, 0] - s[:, 0].min()
     print(f"WG start offsets (cycles): median {np.median(start):.0f}  max {start.max()}  "
           f"WGs starting after 50% of the kernel: {(start > 0.5 * (s[:, -1].max() - s[:, 0].min())).sum()}")
-    sub = st.view(B, 128).cpu().numpy().astype(np.int64)
+    sub = st.view(B, 128).cpu().numpy().astype(np.int64)[rows]
     SUBN = ["K/V projection", "Q projection", "phase A (M)", "top-u select", "phase C (softmax·V)", "phase D (rest)"]
     for c, base in ((0, 100), (1, 108)):
         ss = sub[:, base:base + 7]
