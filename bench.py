@@ -7,6 +7,13 @@ the NMSE_Split reduction of that batch on the device (run_validation's
 ``loss += NMSELossSplit(output, label)``, QuantizationAwareTraining.py:115-122).
 Inputs are synthetic channels resident in HBM; weights are the seeded synthetic recipe.
 
+Two batches are in flight per GPU by default (``--inflight 2``): step k runs on engine lane k mod 2, each
+lane an engine replica (same weights) with its own HIP stream, input batch, resident sampler chain and
+fused-NMSE ticket.  Every step is still one full forward of a 512-sequence batch; the second stream lets the
+next batch's workgroups take the CUs the current launch's early finishers free (the launch's tail: per-
+workgroup time spread ≈ 11 %) instead of waiting for its slowest workgroup.  ``--inflight 1``
+is the one-stream, back-to-back form.
+
 Multi-GPU: ``python bench.py --gpus N`` starts N rank processes itself (torch.distributed.run in a
 child process, before anything touches the GPU); the driver may also launch it under torchrun.
 One process per GPU, each with its own 512-sequence shard of an N×512 global batch (weak scaling,
@@ -133,6 +140,10 @@ def parse_args(argv=None):
                     help="keep warming up (untimed) until this many seconds have passed, so the GPU clock has "
                          "settled even with a short --warmup")
     ap.add_argument("--batch", type=int, default=512, help="sequences per GPU per step")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight per GPU: step k runs on engine lane k mod N, each lane an engine "
+                         "replica with its own HIP stream, inputs, sampler chain and NMSE ticket (every step "
+                         "is still one full B-sequence forward; 1 = one stream, back-to-back launches)")
     ap.add_argument("--snr", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=4,
@@ -223,35 +234,45 @@ def main(argv=None):
     from channelestimationtransformer_amd.engine import nmse_split, nmse_split_sums
     from channelestimationtransformer_amd.flops import informer_flops, io_bytes
 
-    model = build_model(dev)
-    eng = model.engine(dev)
-    eng.set_variant(args.variant)
-    eng.set_sampler(args.sampler == "host")
-    eng.seed(1)                 # every rank draws the same index samples (shared across the batch)
-    B, T = args.batch, CFG["pred_len"]
-    xe_np, xd_np, lab_np = make_batch(B, snr=args.snr, seed=1234 + 7919 * rank)
-    xe = torch.from_numpy(xe_np).to(dev)
-    xd = torch.from_numpy(xd_np).to(dev)
-    lab = torch.from_numpy(lab_np).to(dev)
-    out = torch.empty(B, T, 16, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    B, T, NL = args.batch, CFG["pred_len"], max(1, args.inflight)
     all_sums = torch.zeros(args.steps + 1, 2, T, dtype=torch.float64, device=dev)   # row `steps`: warm-up
     sums = all_sums[:args.steps]
-    fused_step = eng.bind_forward_nmse(xe, xd, out, lab, all_sums, stream)
+    lanes = []
+    for i in range(NL):
+        # lane i: an engine replica (same weights) on its own stream, fed its own synthetic batch
+        model = build_model(dev)
+        eng = model.engine(dev)
+        eng.set_variant(args.variant)
+        eng.set_sampler(args.sampler == "host")
+        eng.seed(1 + i)             # every rank draws the same index samples per lane (shared across the batch)
+        xe_np, xd_np, lab_np = make_batch(B, snr=args.snr, seed=1234 + 7919 * rank + 104729 * i)
+        xe = torch.from_numpy(xe_np).to(dev)
+        xd = torch.from_numpy(xd_np).to(dev)
+        lab = torch.from_numpy(lab_np).to(dev)
+        out = torch.empty(B, T, 16, device=dev)
+        st = torch.cuda.current_stream(dev) if NL == 1 else torch.cuda.Stream(dev)
+        fused = eng.bind_forward_nmse(xe, xd, out, lab, all_sums, st.cuda_stream)
+        lanes.append(dict(model=model, eng=eng, xe=xe, xd=xd, lab=lab, out=out, stream=st, fused=fused,
+                          xe_np=xe_np, xd_np=xd_np))
 
-    def step(k):
-        # forward + NMSE_Split of the batch: one launch (the kernel fuses the reduction into its epilogue)
+    def step(k, lane):
+        # forward + NMSE_Split of one batch on `lane`: one launch (the kernel fuses the reduction into its
+        # epilogue); k < 0: a warm-up step (its sums go to the spare row)
+        ln = lanes[lane % NL]
         if args.nmse == "fused":
-            fused_step(k if k >= 0 else args.steps)
+            ln["fused"](k if k >= 0 else args.steps)
         else:
-            eng.forward(xe, xd, out, None, stream)
-            nmse_split_sums(out, lab, all_sums[k if k >= 0 else args.steps], stream=stream)
+            with torch.cuda.stream(ln["stream"]):
+                ln["eng"].forward(ln["xe"], ln["xd"], ln["out"], None, ln["stream"].cuda_stream)
+                nmse_split_sums(ln["out"], ln["lab"], all_sums[k if k >= 0 else args.steps],
+                                stream=ln["stream"].cuda_stream)
+    eng = lanes[0]["eng"]
 
     t_w = time.perf_counter()
     n_warm = 0
     while n_warm < args.warmup or time.perf_counter() - t_w < args.settle_s:
         for _ in range(64 if n_warm >= args.warmup else 1):
-            step(-1)
+            step(-1, n_warm)
             n_warm += 1
         if n_warm >= args.warmup:
             torch.cuda.synchronize(dev)
@@ -259,10 +280,10 @@ def main(argv=None):
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.timing(True, every=16)     # HIP events around 1 launch in 16 of the timed region
+    eng.timing(True, every=16)     # HIP events around 1 launch in 16 of lane 0's launches (on its stream)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(k)
+        step(k, k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -279,7 +300,8 @@ def main(argv=None):
         dist.all_gather(allt, torch.tensor([dt_rank], dtype=torch.float64, device=dev))
         per_rank = [float(t.item()) for t in allt]
     dt = max(per_rank)
-    nmse, check = collate_and_report(sums, out, lab, world, rank, lambda p, y: nmse_split(p, y))
+    last = lanes[(args.steps - 1) % NL]   # the lane that ran the last timed step
+    nmse, check = collate_and_report(sums, last["out"], last["lab"], world, rank, lambda p, y: nmse_split(p, y))
 
     if rank == 0:
         flops = informer_flops()
@@ -295,12 +317,14 @@ def main(argv=None):
             from oracle.informer_np import InformerConfig, InformerOracle, sample_shapes
 
             idx = draw_indices(sample_shapes(InformerConfig()), seed=5)
+            ln0 = lanes[0]
             eng.set_indices(idx)
             o8 = torch.empty(8, 5, 16, device=dev)
-            eng.forward(xe[:8].contiguous(), xd[:8].contiguous(), o8)
+            eng.forward(ln0["xe"][:8].contiguous(), ln0["xd"][:8].contiguous(), o8)
             torch.cuda.synchronize(dev)
             ref, _ = InformerOracle(InformerConfig(), synthetic_state_dict(
-                informer_stack_spec(16, 16, 16, 128, 8, [4], 3, 64, freq="gelu"), 0)).forward(xe_np[:8], xd_np[:8], idx)
+                informer_stack_spec(16, 16, 16, 128, 8, [4], 3, 64, freq="gelu"), 0)).forward(
+                    ln0["xe_np"][:8], ln0["xd_np"][:8], idx)
             a, r = o8.cpu().numpy().astype(np.float64), ref
             parity = float(np.sum((a - r) ** 2) / np.sum(r ** 2))
         except Exception as exc:  # pragma: no cover - reported, not fatal
@@ -320,7 +344,8 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (seeded Jakes channels, SNR %g dB; seeded synthetic weights)" % args.snr,
             "config": {"workload": WORKLOAD, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"dp{world}", "nmse": args.nmse, "kernel_variant": args.variant},
+                       "parallelism": f"dp{world}", "nmse": args.nmse, "kernel_variant": args.variant,
+                       "inflight_batches_per_gpu": NL},
             "world": world,
             "backend": "nccl" if world > 1 else None,
             "per_rank_ms_per_step": [round(t / args.steps * 1e3, 4) for t in per_rank],
@@ -332,6 +357,10 @@ def main(argv=None):
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name, "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "kernel_ms_note": ("HIP events on lane 0's stream; with %d batches in flight a "
+                                            "launch shares the GPU with its neighbour for part of its span, "
+                                            "so this understates the per-launch rate" % NL) if NL > 1 else None,
+                         "achieved_from_throughput": round(flops * seqs / dt / 1e12, 3),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }

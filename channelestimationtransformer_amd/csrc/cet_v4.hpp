@@ -6,15 +6,25 @@
 //           is hi·hi + hi·lo + lo·hi on three MFMAs (≈16 significant bits per operand, fp32
 //           accumulation): the fp32-parity mode, and the exact carrier of LSQ integer grids whose
 //           |q| exceeds bf16's 256.
-//   P_FP8   OCP e4m3 activations on v_mfma_f32_16x16x32_fp8_fp8 for the LSQ-quantised layers; the
-//           integer weight grid q ∈ [−128, 127] is carried exactly as 16·⌊q/16⌋ and q mod 16 (both
-//           e4m3-exact), two MFMAs per k-step; the step size sits in the epilogue.  The layers the
-//           reference does not quantise (token embedding, projection) and the attention products
-//           stay bf16.
+//   P_FP8   OCP e4m3 activations on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 for the
+//           LSQ-quantised layers.  The integer weight grid q ∈ [−128, 127] is carried exactly as
+//           hi = ⌊q/16⌋ ∈ [−8, 7] and lo = q mod 16 ∈ [0, 15] (both e4m3-exact): one MFMA covers 64
+//           input features, lane groups 0-1 holding hi (E8M0 block scale 2^4) and 2-3 holding lo
+//           (scale 2^0) against the same activations duplicated, so both parts accumulate in one C
+//           with no epilogue rescale; the step size sits in the epilogue.  The layers the reference
+//           does not quantise (token embedding, projection) and the attention products stay bf16.
 //
-// Fragment geometry is the same for every policy (v_mfma_f32_16x16x32_*: lane l holds A[row l&15]
-// [k = 8(l>>4) .. +7] and B[k = 8(l>>4) .. +7][col l&15]), so the GEMM loops are shared; only the
-// element type of a fragment, the number of MFMAs per k-step and the image format change.
+// Fragment geometry: bf16 / split bf16 use v_mfma_f32_16x16x32_* (lane l holds A[row l&15]
+// [k = 8(l>>4) .. +7] and B[k = 8(l>>4) .. +7][col l&15]); fp8 uses the 16x16x128 block-scaled form.
+// Probed on MI355X (tools/probe/mfma_scale_probe.hip, profiles/r03/mfma_scale_probe.txt): byte j of
+// lane l carries K index 16(l>>4) + j for j < 16 and 64 + 16(l>>4) + (j − 16) for j ≥ 16, and scale
+// block b = K/32 of row (col) r takes its E8M0 byte from lane r + 16b — so bytes 0-15 of every lane lie
+// in blocks 0-1 (scales from lanes 0-31) and bytes 16-31 in blocks 2-3 (lanes 32-63).  Bytes 0-15 carry
+// hi (×2^4) and bytes 16-31 lo (×2^0) of the real features 64·kb + 32·((j>>3)&1) + 8(l>>4) + (j&7), in
+// the same byte order in both operands (the products pair up whatever K index a byte denotes), so a
+// lane's activation bytes are two 8-byte runs (k0 and k0 + 32) repeated twice.  The weight blob keeps
+// 16 B per lane per 32-feature k-step for every policy, so the GEMM loops are shared: an fp8 MFMA
+// consumes KR = 2 k-steps of weight fragments (the hi half, then the lo half).
 //
 // Images (LDS): bf16 rows of 288 B (18 16-byte slots: the 16 lanes of every ds_read_b128 lane group
 // hit 16 distinct slots — conflict-free, MI355X_MICROARCH §LDS), X3 adds a lo plane, fp8 rows are
@@ -56,7 +66,7 @@ struct XF<P_X3> {
 };
 template <>
 struct XF<P_FP8> {
-  long q;   // 8 e4m3
+  i32x8 q;   // 32 e4m3: features k0 .. +7 and k0 + 32 .. +7, twice (hi and lo blocks)
 };
 template <int P>
 struct WF {  // A-role (weight) fragment
@@ -68,39 +78,50 @@ struct WF<P_X3> {
 };
 template <>
 struct WF<P_FP8> {
-  long hi, lo;   // 16·⌊q/16⌋ and q mod 16, e4m3
+  i32x4 q;   // 16 of the lane's 32 e4m3 weight bytes of one 64-feature block (hi or lo part)
 };
 
-__device__ __forceinline__ f32x4 mfma8(long a, long b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+// k-steps (32 features of weight fragments) one MFMA consumes, and the lane's activation k offset
+template <int P>
+constexpr int KR = P == P_FP8 ? 2 : 1;
+template <int P>
+__device__ __forceinline__ int kq_of(int lane) {
+  return 8 * (lane >> 4);
 }
 
-// W·X (weights as A): the transposed dense layer Yᵀ = W·Xᵀ
+// E8M0 block scales of the weight operand: lanes 0-31 give blocks 0-1 (bytes 0-15: hi = ⌊q/16⌋, ×2^4),
+// lanes 32-63 blocks 2-3 (bytes 16-31: lo, ×2^0)
+__device__ __forceinline__ int fp8_wscale() { return (threadIdx.x & 32) ? 127 : 131; }
+__device__ __forceinline__ i32x8 cat8(const i32x4& a, const i32x4& b) {
+  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// W·X (weights as A): the transposed dense layer Yᵀ = W·Xᵀ; a points at KR<P> weight fragments
 template <int P>
-__device__ __forceinline__ f32x4 mma(const WF<P>& a, const XF<P>& b, f32x4 c) {
+__device__ __forceinline__ f32x4 mma(const WF<P>* a, const XF<P>& b, f32x4 c) {
   if constexpr (P == P_BF16) {
-    return mfma16x16x32(a.h, b.h, c);
+    return mfma16x16x32(a->h, b.h, c);
   } else if constexpr (P == P_X3) {
-    c = mfma16x16x32(a.l, b.h, c);   // small terms first
-    c = mfma16x16x32(a.h, b.l, c);
-    return mfma16x16x32(a.h, b.h, c);
+    c = mfma16x16x32(a->l, b.h, c);   // small terms first
+    c = mfma16x16x32(a->h, b.l, c);
+    return mfma16x16x32(a->h, b.h, c);
   } else {
-    c = mfma8(a.lo, b.q, c);
-    return mfma8(a.hi, b.q, c);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(a[0].q, a[1].q), b.q, c, 0, 0, 0, fp8_wscale(), 0,
+                                                            127);
   }
 }
 // X·Wᵀ (activations as A): V = X·Wvᵀ, whose C fragment is the A operand of Oᵀ = Vᵀ·Pᵀ
 template <int P>
-__device__ __forceinline__ f32x4 mma_xw(const XF<P>& a, const WF<P>& b, f32x4 c) {
+__device__ __forceinline__ f32x4 mma_xw(const XF<P>& a, const WF<P>* b, f32x4 c) {
   if constexpr (P == P_BF16) {
-    return mfma16x16x32(a.h, b.h, c);
+    return mfma16x16x32(a.h, b->h, c);
   } else if constexpr (P == P_X3) {
-    c = mfma16x16x32(a.l, b.h, c);
-    c = mfma16x16x32(a.h, b.l, c);
-    return mfma16x16x32(a.h, b.h, c);
+    c = mfma16x16x32(a.l, b->h, c);
+    c = mfma16x16x32(a.h, b->l, c);
+    return mfma16x16x32(a.h, b->h, c);
   } else {
-    c = mfma8(a.q, b.lo, c);
-    return mfma8(a.q, b.hi, c);
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.q, cat8(b[0].q, b[1].q), c, 0, 0, 0, 127, 0,
+                                                            fp8_wscale());
   }
 }
 
@@ -178,7 +199,9 @@ struct Img : ImgBase<P> {
     constexpr int RS = Geo<P>::RS;
     XF<P> r;
     if constexpr (P == P_FP8) {
-      r.q = *reinterpret_cast<const long*>(base + row * RS + k0);
+      const i32x2 a = *reinterpret_cast<const i32x2*>(base + row * RS + k0);
+      const i32x2 b = *reinterpret_cast<const i32x2*>(base + row * RS + k0 + 32);
+      r.q = i32x8{a[0], a[1], b[0], b[1], a[0], a[1], b[0], b[1]};
     } else {
       r.h = *reinterpret_cast<const bf16x8*>(base + row * RS + 2 * k0);
       if constexpr (P == P_X3) r.l = *reinterpret_cast<const bf16x8*>(base + lo + row * RS + 2 * k0);
@@ -282,8 +305,7 @@ __device__ __forceinline__ WF<P> wfrag(const Mem& m, uint32_t off, int lane) {
   WF<P> r;
   const uint4 v = wload16(m, off, lane);
   if constexpr (P == P_FP8) {
-    r.hi = (long)(((unsigned long long)v.y << 32) | v.x);
-    r.lo = (long)(((unsigned long long)v.w << 32) | v.z);
+    r.q = __builtin_bit_cast(i32x4, v);
   } else {
     r.h = __builtin_bit_cast(bf16x8, v);
     if constexpr (P == P_X3) r.l = __builtin_bit_cast(bf16x8, wload16(m, off + m.wlo, lane));
@@ -347,13 +369,13 @@ template <int P, int KS, int N, class BL, class Epi>
 __device__ __forceinline__ void gemm_res(const WPre<P, KS>& p, int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_op(), w = wave_id();
   const int n0 = 16 * w + (lane >> 4) * 4;
-  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int kq = kq_of<P>(lane), mrow = lane & 15;
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) c = mma<P>(p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+      for (int ks = 0; ks < KS; ks += KR<P>) c = mma<P>(&p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
       epi(mt, n0, c * p.sc + p.bi);
     }
   }
@@ -368,24 +390,24 @@ template <int P, int KS, int NMT, class BL, class Epi>
 __device__ __forceinline__ void gemm_res_n(const WPre<P, KS>& p, BL&& bl, Epi&& epi) {
   const int lane = lane_op(), w = wave_id();
   const int n0 = 16 * w + (lane >> 4) * 4;
-  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int kq = kq_of<P>(lane), mrow = lane & 15;
   XF<P> b[KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) b[ks] = bl(mrow, ks * 32 + kq);
+  for (int ks = 0; ks < KS; ks += KR<P>) b[ks] = bl(mrow, ks * 32 + kq);
 #pragma unroll
   for (int mt = 0; mt < NMT; ++mt) {
     XF<P> bn[KS];
     if (mt + 1 < NMT) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bn[ks] = bl((mt + 1) * 16 + mrow, ks * 32 + kq);
+      for (int ks = 0; ks < KS; ks += KR<P>) bn[ks] = bl((mt + 1) * 16 + mrow, ks * 32 + kq);
     }
     f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) c = mma<P>(p.a[ks], b[ks], c);
+    for (int ks = 0; ks < KS; ks += KR<P>) c = mma<P>(&p.a[ks], b[ks], c);
     epi(mt, n0, c * p.sc + p.bi);
     if (mt + 1 < NMT) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) b[ks] = bn[ks];
+      for (int ks = 0; ks < KS; ks += KR<P>) b[ks] = bn[ks];
     }
   }
 }
@@ -398,7 +420,7 @@ __device__ __forceinline__ void gemm_res_n(const Mem& m, const GemmDesc d, BL&& 
 template <int P, int KS, class BL, class Epi>
 __device__ __forceinline__ void gemm_tiles(const Mem& m, const GemmDesc d, int n_tiles, int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_op(), w = wave_id();
-  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int kq = kq_of<P>(lane), mrow = lane & 15;
   int nt0 = w, nt_step = NW, mt0 = 0, mt_step = 1;
   if (n_tiles < NW) {
     const int per = NW / n_tiles;
@@ -417,7 +439,7 @@ __device__ __forceinline__ void gemm_tiles(const Mem& m, const GemmDesc d, int n
     for (int mt = mt0; mt < nmt; mt += mt_step) {
       f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) c = mma<P>(a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+      for (int ks = 0; ks < KS; ks += KR<P>) c = mma<P>(&a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
       epi(mt, n0, c * sc + bi);
     }
   }
@@ -436,7 +458,7 @@ __device__ __forceinline__ WPre<P, KS> prefetch_tiles(const Mem& m, const GemmDe
 template <int P, int KS, class BL, class Epi>
 __device__ __forceinline__ void gemm_tiles1(const WPre<P, KS>& p, int n_tiles, int nmt, BL&& bl, Epi&& epi) {
   const int lane = lane_op(), w = wave_id();
-  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int kq = kq_of<P>(lane), mrow = lane & 15;
   const int per = NW / n_tiles;
   if (w >= per * n_tiles) return;
   const int nt = w % n_tiles, mt_step = per;
@@ -444,7 +466,7 @@ __device__ __forceinline__ void gemm_tiles1(const WPre<P, KS>& p, int n_tiles, i
   for (int mt = w / n_tiles; mt < nmt; mt += mt_step) {
     f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) c = mma<P>(p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
+    for (int ks = 0; ks < KS; ks += KR<P>) c = mma<P>(&p.a[ks], bl(mt * 16 + mrow, ks * 32 + kq), c);
     epi(mt, n0, c * p.sc + p.bi);
   }
 }
@@ -464,9 +486,9 @@ __device__ __forceinline__ WPre<P, KH> prefetch_kouter(const Mem& m, const GemmD
 template <int P, int KS, int KH, int NMT, class BL, class Epi>
 __device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem& m, const GemmDesc d, BL&& bl,
                                                 Epi&& epi) {
-  static_assert(KS % KH == 0, "k-steps split into equal groups");
+  static_assert(KS % KH == 0 && KH % KR<P> == 0, "k-steps split into equal groups");
   const int lane = lane_op(), w = wave_id();
-  const int kq = (lane >> 4) * 8, mrow = lane & 15;
+  const int kq = kq_of<P>(lane), mrow = lane & 15;
   const int n0 = 16 * w + (lane >> 4) * 4;
   const f32x4 sc = p.sc, bi = p.bi;
   f32x4 c[NMT];
@@ -483,16 +505,16 @@ __device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem&
 #pragma unroll
     for (int ks = 0; ks < KH; ++ks) a[ks] = hf == 0 ? p.a[ks] : wfrag<P>(m, t0 + (uint32_t)(hf * KH + ks) * 1024u, lane);
 #pragma unroll
-    for (int ks = 0; ks < KH; ++ks) {
+    for (int ks = 0; ks < KH; ks += KR<P>) {
       const int kk = hf * KH + ks;
       XF<P> bn[NMT];
-      if (kk + 1 < KS) {
+      if (kk + KR<P> < KS) {
 #pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) bn[mt] = bl(mt * 16 + mrow, (kk + 1) * 32 + kq);
+        for (int mt = 0; mt < NMT; ++mt) bn[mt] = bl(mt * 16 + mrow, (kk + KR<P>) * 32 + kq);
       }
 #pragma unroll
-      for (int mt = 0; mt < NMT; ++mt) c[mt] = mma<P>(a[ks], b[mt], c[mt]);
-      if (kk + 1 < KS) {
+      for (int mt = 0; mt < NMT; ++mt) c[mt] = mma<P>(&a[ks], b[mt], c[mt]);
+      if (kk + KR<P> < KS) {
 #pragma unroll
         for (int mt = 0; mt < NMT; ++mt) b[mt] = bn[mt];
       }
@@ -746,7 +768,7 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, i
   const int col = lane & 15, g = lane >> 4;
   const int nkt = (io.LK + 15) >> 4;
   const int fq = 16 * h + 4 * g;
-  const int kq = g * 8;
+  const int kq = kq_of<PD>(lane);
   WF<PD> wk[4], wv[4];
   load_frags<PD, 4>(m, io.wk, h, wk);
   load_frags<PD, 4>(m, io.wv, h, wv);
@@ -761,10 +783,10 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, i
     if (mt < nkt) {
       f32x4 k = {0.f, 0.f, 0.f, 0.f}, v = k;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < 4; ks += KR<PD>) {
         const XF<PD> bx = io.xkv.ld(mt * 16 + col, ks * 32 + kq);
-        k = mma<PD>(wk[ks], bx, k);
-        v = mma_xw<PD>(bx, wv[ks], v);
+        k = mma<PD>(&wk[ks], bx, k);
+        v = mma_xw<PD>(bx, &wv[ks], v);
       }
       Kf[mt] = split4<PA>(k * sk + bk);
       Vf[mt] = split4<PA>(v * sv + bv);
@@ -791,7 +813,7 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
   };
   SUB(0);
   const int fq = 16 * h + 4 * g;
-  const int kq = g * 8;
+  const int kq = kq_of<PD>(lane);
   AF<PA> Kf[MK], Vf[MK];
   // single-tile heads (the decoder's, and the last encoder layer's): few live registers, so the Q
   // weights could be requested with the K/V weights (one L2 round trip instead of two in sequence);
@@ -826,7 +848,7 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
   auto project_q = [&](int row) __attribute__((always_inline)) {
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) q = mma<PD>(wq[ks], io.xq.ld(row, ks * 32 + kq), q);
+    for (int ks = 0; ks < 4; ks += KR<PD>) q = mma<PD>(&wq[ks], io.xq.ld(row, ks * 32 + kq), q);
     return split4<PA>(q * sq + bq);
   };
 

@@ -78,7 +78,7 @@ __device__ __forceinline__ void gemm_res_s(const WPre<P, KS>& p, int nmt, BL&& b
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) c[s] = mma<P>(p.a[ks], bl(s, mt * 16 + mrow, ks * 32 + kq), c[s]);
+        for (int s = 0; s < NS; ++s) c[s] = mma<P>(&p.a[ks], bl(s, mt * 16 + mrow, ks * 32 + kq), c[s]);
 #pragma unroll
       for (int s = 0; s < NS; ++s) epi(s, mt, n0, c[s] * p.sc + p.bi);
     }
@@ -102,7 +102,7 @@ __device__ __forceinline__ void gemm_tiles1_s(const WPre<P, KS>& p, int n_tiles,
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) c[s] = mma<P>(p.a[ks], bl(s, mt * 16 + mrow, ks * 32 + kq), c[s]);
+      for (int s = 0; s < NS; ++s) c[s] = mma<P>(&p.a[ks], bl(s, mt * 16 + mrow, ks * 32 + kq), c[s]);
 #pragma unroll
     for (int s = 0; s < NS; ++s) epi(s, mt, n0, c[s] * p.sc + p.bi);
   }
@@ -125,7 +125,7 @@ __device__ __forceinline__ void gemm_tiles_s(const Mem& m, const GemmDesc d, int
     epi_vecs(m, d, n0, sc, bi);
     f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) c = mma<P>(a[ks], bl(s, mt * 16 + mrow, ks * 32 + kq), c);
+    for (int ks = 0; ks < KS; ++ks) c = mma<P>(&a[ks], bl(s, mt * 16 + mrow, ks * 32 + kq), c);
     epi(s, mt, n0, c * sc + bi);
   }
 }
@@ -168,7 +168,7 @@ __device__ __forceinline__ void gemm_kouter_s(const WPre<P, KH>& p, const Mem& m
 #pragma unroll
       for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-        for (int s = 0; s < NS; ++s) c[s][mt] = mma<P>(a[ks], b[s][mt], c[s][mt]);
+        for (int s = 0; s < NS; ++s) c[s][mt] = mma<P>(&a[ks], b[s][mt], c[s][mt]);
       if (kk + 1 < KS) {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
@@ -299,8 +299,8 @@ __device__ __forceinline__ void project_kv_s(const HeadIO2<PD, NS>& io, const Me
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const XF<PD> bx = io.xkv[s].ld(mt * 16 + col, ks * 32 + kq);
-          k[s] = mma<PD>(wk[ks], bx, k[s]);
-          v[s] = mma_xw<PD>(bx, wv[ks], v[s]);
+          k[s] = mma<PD>(&wk[ks], bx, k[s]);
+          v[s] = mma_xw<PD>(bx, &wv[ks], v[s]);
         }
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
@@ -344,7 +344,7 @@ __device__ __forceinline__ void attention_s(const HeadIO2<PD, NS>& io, const Mem
   auto project_q = [&](int s, int row) __attribute__((always_inline)) {
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) q = mma<PD>(wq[ks], io.xq[s].ld(row, ks * 32 + kq), q);
+    for (int ks = 0; ks < 4; ++ks) q = mma<PD>(&wq[ks], io.xq[s].ld(row, ks * 32 + kq), q);
     return split4<PA>(q * sq + bq);
   };
 

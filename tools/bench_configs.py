@@ -4,6 +4,11 @@
   C5    InformerStackLSQ 8-bit weights (QuantizationStudy/LSQ), B=1024: bf16 activations (exact integer
         grid) and fp8 e4m3 activations on the fp8 MFMA (roofline fraction against the fp8 peak)
   full  FullPrecision InformerStack attn="full", e_layers=[4,3] (the TimingAnalysis shape), B=512
+  d64   the architecture of the reference's only trained weights (MimoSimulation/models/checkpoint/
+        checkpoint.pth, loaded by MimoSimulation/Predict.py:91-93: InformerStack(16,16,16, 25,10,5, 5,
+        d_model 64, 8 heads, e_layers [4,3], 3, d_ff 64, attn "full")), B=512, seeded synthetic weights of
+        that architecture (the checkpoint never leaves the reference tree); d_model 64 runs on the
+        layer-wise engine
 
 Seeded synthetic weights, seeded synthetic channel features resident in HBM.  Kernel time: the
 engine's HIP events around one launch in 8 (same stream), after a ≥1 s clock-settling warm-up.
@@ -34,11 +39,12 @@ from channelestimationtransformer_amd.weights import synthetic_state_dict  # noq
 from oracle.informer_np import InformerConfig, InformerOracle, sample_shapes  # noqa: E402
 from oracle.transformer_np import TransformerConfig, TransformerOracle  # noqa: E402
 
-PEAK = {"bf16": 2500.0, "fp8": 5000.0}   # dense MFMA TFLOP/s (MI355X_MICROARCH.md chip table)
+PEAK = {"bf16": 2500.0, "fp8": 5000.0, "fp32": 157.3}   # dense MFMA TFLOP/s (MI355X_MICROARCH.md chip table)
 
 
-def informer(dev, e_layers, attn, lsq_bits=0):
-    args = [16, 16, 16, 90, 10, 5, 5, 128, 8, e_layers, 3, 64, 0.05, attn, "fixed", "gelu", False, True, dev]
+def informer(dev, e_layers, attn, lsq_bits=0, seq_len=90, d_model=128):
+    args = [16, 16, 16, seq_len, 10, 5, 5, d_model, 8, e_layers, 3, 64, 0.05, attn, "fixed", "gelu", False, True,
+            dev]
     m = InformerStackLSQ(*args, lsq_bits) if lsq_bits else InformerStack(*args)
     spec = m._schema()
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(spec, 0).items()},
@@ -46,7 +52,8 @@ def informer(dev, e_layers, attn, lsq_bits=0):
     if lsq_bits:
         m.enable_lsq(lsq_bits)
     state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
-    orc = InformerOracle(InformerConfig(e_layers=tuple(e_layers), attn=attn, lsq_bits=lsq_bits or None), state)
+    orc = InformerOracle(InformerConfig(seq_len=seq_len, d_model=d_model, e_layers=tuple(e_layers), attn=attn,
+                                        lsq_bits=lsq_bits or None), state)
     return m.eval(), orc
 
 
@@ -64,7 +71,8 @@ def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0):
         eng.set_variant(variant)
     if precision is not None:
         eng.set_precision(precision)
-    xe_np, xd_np, _ = make_batch(B, seed=7)
+    xe_np, xd_np, _ = make_batch(B, seed=7, seq_len=orc.cfg.seq_len) if isinstance(orc, InformerOracle) else \
+        make_batch(B, seed=7)
     xe, xd = torch.from_numpy(xe_np).to(dev), torch.from_numpy(xd_np).to(dev)
     out = torch.empty(B, 5, 16, device=dev)
     prob = bool(eng.prob_calls())
@@ -120,7 +128,11 @@ def main():
          informer_flops(), dict(precision="fp8"), "fp8"),
         ("FullPrecision InformerStack attn=full, e_layers=[4,3]", lambda: informer(dev, [4, 3], "full"), 512,
          informer_flops(e_layers=(4, 3), attn="full"), {}, "bf16"),
+        ("d64 MimoSimulation checkpoint architecture (d_model 64, seq_len 25, e_layers=[4,3], attn=full), "
+         "layer-wise engine", lambda: informer(dev, [4, 3], "full", seq_len=25, d_model=64), 512,
+         informer_flops(seq_len=25, d_model=64, e_layers=(4, 3), attn="full"), {}, "fp32"),
     ]
+    tol = {"fp8": 2e-3}   # rel-NMSE bar: north_star's 1e-4, the self-set fp8 bar for C5 fp8
     for name, mk, B, flops, kw, peak in runs:
         if args.only not in name:
             continue
@@ -130,7 +142,8 @@ def main():
         print(json.dumps({"config": name, "batch": B, "precision": prec, "seq_per_s": round(B / (step_ms * 1e-3), 1),
                           "ms_per_step": round(step_ms, 4), "kernel_ms": round(kern_ms, 4),
                           "flops_per_seq": flops, "tflops": round(tf, 2), "peak_tflops": PEAK[peak],
-                          "mfma_frac": round(tf / PEAK[peak], 4), "parity_rel_nmse_vs_oracle": parity}), flush=True)
+                          "mfma_frac": round(tf / PEAK[peak], 4), "parity_rel_nmse_vs_oracle": parity,
+                          "parity_tolerance": tol.get(peak, 1e-4)}), flush=True)
 
 
 if __name__ == "__main__":
