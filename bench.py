@@ -357,10 +357,14 @@ def main(argv=None):
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name, "kernel_ms": round(avg_kernel_s * 1e3, 4),
-                         "kernel_ms_note": ("HIP events on lane 0's stream; with %d batches in flight a "
-                                            "launch shares the GPU with its neighbour for part of its span, "
-                                            "so this understates the per-launch rate" % NL) if NL > 1 else None,
+                         "kernel_ms_note": ("HIP events on lane 0's stream over the timed region; with %d "
+                                            "batches in flight every launch shares the GPU with its "
+                                            "neighbours for most of its span, so the launch duration is "
+                                            "about %d x the per-batch GPU time and frac understates the "
+                                            "kernel; frac_effective divides the algorithmic FLOPs by the "
+                                            "step time instead" % (NL, NL)) if NL > 1 else None,
                          "achieved_from_throughput": round(flops * seqs / dt / 1e12, 3),
+                         "frac_effective": round(flops * seqs / dt / 1e12 / PEAK_BF16_TFLOPS, 5),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),
                          "hbm_achieved_gbps": round(io_bytes() * B / avg_kernel_s / 1e9, 2)},
         }

@@ -12,6 +12,8 @@
 
 Seeded synthetic weights, seeded synthetic channel features resident in HBM.  Kernel time: the
 engine's HIP events around one launch in 8 (same stream), after a ≥1 s clock-settling warm-up.
+``seq_per_s_two_in_flight``: the same forward with two batches in flight (a second engine replica on its
+own stream, steps alternating), as ``bench.py`` runs C2.
 Parity: the same engine with explicit ProbSparse draws on 16 sequences of the batch against the
 float64 oracle (rel-NMSE).  One JSON line per config.
 
@@ -65,7 +67,7 @@ def transformer(dev):
     return m.eval(), TransformerOracle(TransformerConfig(), state)
 
 
-def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0):
+def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0, m2=None):
     eng = m.engine(dev)
     if variant is not None:
         eng.set_variant(variant)
@@ -96,6 +98,29 @@ def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0):
     ms, k = eng.timing_read()
     eng.timing(False)
     assert torch.isfinite(out).all()
+    # two batches in flight (as bench.py): a second engine replica on its own stream, steps alternating
+    step2_ms = None
+    if m2 is not None:
+        eng2 = m2.engine(dev)
+        if variant is not None:
+            eng2.set_variant(variant)
+        if precision is not None:
+            eng2.set_precision(precision)
+        if prob:
+            eng2.seed(2)
+        out2 = torch.empty(B, 5, 16, device=dev)
+        lanes = [(eng, out, torch.cuda.Stream(dev)), (eng2, out2, torch.cuda.Stream(dev))]
+        for i in range(64):
+            e_, o_, s_ = lanes[i % 2]
+            e_.forward(xe, xd, o_, None, s_.cuda_stream)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            e_, o_, s_ = lanes[i % 2]
+            e_.forward(xe, xd, o_, None, s_.cuda_stream)
+        torch.cuda.synchronize(dev)
+        step2_ms = (time.perf_counter() - t0) * 1e3 / steps
+        assert torch.isfinite(out2).all()
     # parity of this engine (explicit draws) on 16 sequences of the batch
     idx = draw_indices(sample_shapes(orc.cfg), seed=3) if prob else None
     if prob:
@@ -110,7 +135,7 @@ def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0):
     a = o16.cpu().numpy().astype(np.float64)
     parity = float(np.sum((a - ref) ** 2) / np.sum(ref ** 2))
     prec = eng.precision() if hasattr(eng, "precision") and eng.kind == "informer" else "bf16"
-    return ev0.elapsed_time(ev1) / steps, ms / max(k, 1), parity, prec
+    return ev0.elapsed_time(ev1) / steps, ms / max(k, 1), parity, prec, step2_ms
 
 
 def main():
@@ -137,13 +162,16 @@ def main():
         if args.only not in name:
             continue
         m, orc = mk()
-        step_ms, kern_ms, parity, prec = run(m, orc, dev, B, args.steps, **kw)
+        m2 = mk()[0] if "layer-wise" not in name else None
+        step_ms, kern_ms, parity, prec, step2_ms = run(m, orc, dev, B, args.steps, m2=m2, **kw)
         tf = flops * B / (kern_ms * 1e-3) / 1e12
         print(json.dumps({"config": name, "batch": B, "precision": prec, "seq_per_s": round(B / (step_ms * 1e-3), 1),
                           "ms_per_step": round(step_ms, 4), "kernel_ms": round(kern_ms, 4),
                           "flops_per_seq": flops, "tflops": round(tf, 2), "peak_tflops": PEAK[peak],
                           "mfma_frac": round(tf / PEAK[peak], 4), "parity_rel_nmse_vs_oracle": parity,
-                          "parity_tolerance": tol.get(peak, 1e-4)}), flush=True)
+                          "parity_tolerance": tol.get(peak, 1e-4),
+                          "seq_per_s_two_in_flight": round(B / (step2_ms * 1e-3), 1) if step2_ms else None}),
+              flush=True)
 
 
 if __name__ == "__main__":
