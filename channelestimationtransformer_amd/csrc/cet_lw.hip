@@ -29,9 +29,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
 // ------------------------------------------------------------------------------------ GEMM
-// C[m][n] = epi(Σ_k A(m, k) · W[n][k]); 64 × 64 output tile per 256-thread workgroup, K in steps of
-// 16 staged through LDS; wave w computes rows 16w..16w+15 × the tile's 64 columns (4 accumulators).
-constexpr int GT = 64, GK = 16;
+// C[m][n] = epi(Σ_k A(m, k) · W[n][k]); 64 × 64 output tile per 256-thread workgroup; wave w computes
+// rows 16w..16w+15 × the tile's 64 columns (4 accumulators).  K is staged through LDS in chunks of 32:
+// each thread fetches two 4-float runs of A and two of W per chunk (vector loads where the rows allow),
+// the next chunk's runs are in registers while this chunk's MFMAs run, one barrier pair per chunk.
+// LDS rows are 34 floats: the MFMA reads (lanes 0-15: rows r, column k; lanes 16-31: rows r, k + 1)
+// hit 32 distinct banks.
+constexpr int GT = 64, GK = 32, GKS = GK + 2;
 
 __device__ __forceinline__ float load_a(const GemmOp& op, int m, int k) {
   if (m >= op.M || k >= op.K) return 0.f;
@@ -43,25 +47,81 @@ __device__ __forceinline__ float load_a(const GemmOp& op, int m, int k) {
   r = r < 0 ? r + op.L : (r >= op.L ? r - op.L : r);
   return op.A[((size_t)b * op.Ls + op.off + r) * op.lda + c];
 }
+// A row of the GEMM as a fetch sees it: row m = b·L + t split once (the divisions stay out of the K loop)
+struct ARow {
+  int m, b, t;
+};
+__device__ __forceinline__ ARow arow(const GemmOp& op, int m) {
+  const int b = m / op.L;
+  return ARow{m, b, m - b * op.L};
+}
+// four consecutive k of row m (k0 a multiple of 4): one 16-byte load when the run is inside the row and
+// aligned (lda % 4 == 0), else element by element.  amode 1 (circular k=3 conv): the run stays inside one
+// tap (Cin % 4 == 0), so it is four consecutive channels of one source row.
+__device__ __forceinline__ f32x4 load_a4(const GemmOp& op, const ARow& ra, int k0, bool vec) {
+  if (ra.m >= op.M || k0 >= op.K) return f32x4{0.f, 0.f, 0.f, 0.f};
+  if (op.amode == 0) {
+    const float* p = op.A + (size_t)ra.m * op.lda + k0;
+    if (vec && k0 + 3 < op.K) return *reinterpret_cast<const f32x4*>(p);
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = k0 + i < op.K ? p[i] : 0.f;
+    return v;
+  }
+  const int tap = k0 / op.Cin, c = k0 - tap * op.Cin;
+  int r = ra.t - 1 + tap;
+  r = r < 0 ? r + op.L : (r >= op.L ? r - op.L : r);
+  const float* p = op.A + ((size_t)ra.b * op.Ls + op.off + r) * op.lda + c;
+  if (vec && (op.Cin & 3) == 0 && k0 + 3 < op.K) return *reinterpret_cast<const f32x4*>(p);
+  f32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = load_a(op, ra.m, k0 + i);
+  return v;
+}
+__device__ __forceinline__ f32x4 load_w4(const GemmOp& op, int n, int k0, bool vec) {
+  if (n >= op.N) return f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* w = op.W + (size_t)n * op.K;
+  if (vec && k0 + 3 < op.K) return *reinterpret_cast<const f32x4*>(w + k0);
+  f32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = k0 + i < op.K ? w[k0 + i] : 0.f;
+  return r;
+}
 
 __global__ void __launch_bounds__(256) lw_gemm(GemmOp op) {
-  __shared__ float As[GT][GK + 1];
-  __shared__ float Ws[GT][GK + 1];
+  __shared__ float As[GT][GKS];
+  __shared__ float Ws[GT][GKS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int m0 = blockIdx.x * GT, n0 = blockIdx.y * GT;
+  const bool avec = (op.lda & 3) == 0 && ((reinterpret_cast<uintptr_t>(op.A) & 15) == 0);
+  const bool wvec = (op.K & 3) == 0 && ((reinterpret_cast<uintptr_t>(op.W) & 15) == 0);
+  // this thread's runs: row (tid >> 3) and (tid >> 3) + 32, columns 4·(tid & 7) .. +3 of the chunk
+  const int fr = tid >> 3, fc = 4 * (tid & 7);
+  const ARow far[2] = {arow(op, m0 + fr), arow(op, m0 + fr + 32)};
+  f32x4 ra[2], rw[2];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ra[i] = load_a4(op, far[i], k0 + fc, avec);
+      rw[i] = load_w4(op, n0 + fr + 32 * i, k0 + fc, wvec);
+    }
+  };
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  fetch(0);
   for (int k0 = 0; k0 < op.K; k0 += GK) {
-    // 64 × 16 of A and of W: 1024 elements each, 4 per thread
+    __syncthreads();   // the previous chunk has been read
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i, r = e >> 4, c = e & 15;
-      As[r][c] = load_a(op, m0 + r, k0 + c);
-      const int n = n0 + r, k = k0 + c;
-      Ws[r][c] = n < op.N && k < op.K ? op.W[(size_t)n * op.K + k] : 0.f;
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        As[fr + 32 * i][fc + c] = ra[i][c];
+        Ws[fr + 32 * i][fc + c] = rw[i][c];
+      }
     }
     __syncthreads();
+    if (k0 + GK < op.K) fetch(k0 + GK);
 #pragma unroll
     for (int kk = 0; kk < GK; kk += 4) {
       const float a = As[16 * w + (lane & 15)][kk + (lane >> 4)];
@@ -71,26 +131,89 @@ __global__ void __launch_bounds__(256) lw_gemm(GemmOp op) {
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
       }
     }
-    __syncthreads();
   }
-  // epilogue: lane holds rows 4(lane>>4)+r of the wave's 16, column lane&15 of each 16-wide group
+  // epilogue: lane holds rows 4(lane>>4)+r of the wave's 16, column lane&15 of each 16-wide group.
+  // Every epilogue operand (scale, bias, positional row, residual) is loaded before the first store:
+  // Y may alias R (in-place residual), so a load placed after a store cannot be hoisted above it, and
+  // the 16 dependent L2 round trips per lane were most of the kernel's time.
+  float pv[4][4], rv[4][4], sc[4], bi[4];
+  ARow er[4];   // the lane's four output rows, split once
+#pragma unroll
+  for (int r = 0; r < 4; ++r) er[r] = arow(op, m0 + 16 * w + 4 * (lane >> 4) + r);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + 16 * j + (lane & 15);
+    const bool nv = n < op.N;
+    sc[j] = nv && op.scale ? op.scale[n] : 1.f;
+    bi[j] = nv && op.bias ? op.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = er[r].m;
+      const bool v = nv && m < op.M;
+      pv[j][r] = v && op.pe ? op.pe[(size_t)er[r].t * op.N + n] : 0.f;
+      rv[j][r] = v && op.R ? op.R[(size_t)m * op.ldr + n] : 0.f;
+    }
+  }
+  if (op.ln_g) {
+    // x + sublayer(x) of whole rows (N ≤ 64: n0 = 0, the tile holds every column), then the LayerNorm
+    // the next layer reads (in place: the pre-norm sum is not read again)
+    float y[4][4], gg[4], bb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = 16 * j + (lane & 15);
+      const bool nv = n < op.N;
+      gg[j] = nv ? op.ln_g[n] : 0.f;
+      bb[j] = nv ? op.ln_b[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[j][r] * sc[j] + bi[j];
+        if (op.pe) v += pv[j][r];
+        if (op.act == 1) v = gelu(v);
+        else if (op.act == 2) v = fmaxf(v, 0.f);
+        else if (op.act == 3) v = v > 0.f ? v : expm1f(v);
+        if (op.R) v += rv[j][r];
+        y[j][r] = nv ? v : 0.f;
+      }
+    }
+    const float invN = 1.0f / (float)op.N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s = (y[0][r] + y[1][r]) + (y[2][r] + y[3][r]);
+      for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);   // the 16 lanes of row r
+      const float mean = s * invN;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = 16 * j + (lane & 15) < op.N ? y[j][r] - mean : 0.f;
+        q = fmaf(d, d, q);
+      }
+      for (int o = 8; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
+      const float inv = 1.0f / sqrtf(q * invN + 1e-5f);
+      const int m = er[r].m;
+      if (m >= op.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 16 * j + (lane & 15);
+        if (n < op.N) op.Y[(size_t)m * op.ldy + n] = (y[j][r] - mean) * inv * gg[j] + bb[j];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + 16 * j + (lane & 15);
     if (n >= op.N) continue;
-    const float sc = op.scale ? op.scale[n] : 1.f;
-    const float bi = op.bias ? op.bias[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = m0 + 16 * w + 4 * (lane >> 4) + r;
+      const int m = er[r].m;
       if (m >= op.M) continue;
-      float y = acc[j][r] * sc + bi;
-      const int b = m / op.L, t = m - b * op.L;
-      if (op.pe) y += op.pe[(size_t)t * op.N + n];
+      float y = acc[j][r] * sc[j] + bi[j];
+      const int b = er[r].b, t = er[r].t;
+      if (op.pe) y += pv[j][r];
       if (op.act == 1) y = gelu(y);
       else if (op.act == 2) y = fmaxf(y, 0.f);
       else if (op.act == 3) y = y > 0.f ? y : expm1f(y);
-      if (op.R) y += op.R[(size_t)m * op.ldr + n];
+      if (op.R) y += rv[j][r];
       if (op.row_t0 > 0) {   // keep rows t ≥ t0 of every sequence, written as [b][t − t0]
         if (t < op.row_t0) continue;
         op.Y[((size_t)b * (op.L - op.row_t0) + (t - op.row_t0)) * op.ldy + n] = y;
@@ -153,17 +276,25 @@ __global__ void __launch_bounds__(256) lw_gemm_s(GemmOp op) {
   if (n >= op.N) return;
   const float sc = op.scale ? op.scale[n] : 1.f;
   const float bi = op.bias ? op.bias[n] : 0.f;
+  float pv[4], rv[4];   // loaded before the first store (Y may alias R), as in lw_gemm
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + 4 * (lane >> 4) + r;
+    const bool v = m < op.M;
+    pv[r] = v && op.pe ? op.pe[(size_t)(m - (m / op.L) * op.L) * op.N + n] : 0.f;
+    rv[r] = v && op.R ? op.R[(size_t)m * op.ldr + n] : 0.f;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + 4 * (lane >> 4) + r;
     if (m >= op.M) continue;
     float y = acc[r] * sc + bi;
     const int b = m / op.L, t = m - b * op.L;
-    if (op.pe) y += op.pe[(size_t)t * op.N + n];
+    if (op.pe) y += pv[r];
     if (op.act == 1) y = gelu(y);
     else if (op.act == 2) y = fmaxf(y, 0.f);
     else if (op.act == 3) y = y > 0.f ? y : expm1f(y);
-    if (op.R) y += op.R[(size_t)m * op.ldr + n];
+    if (op.R) y += rv[r];
     if (op.row_t0 > 0) {
       if (t < op.row_t0) continue;
       op.Y[((size_t)b * (op.L - op.row_t0) + (t - op.row_t0)) * op.ldy + n] = y;
@@ -260,6 +391,7 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
   // ---- S = Q·Kᵀ, tile (qt, kt) owned by wave (qt·nkt + kt) mod 4, accumulated in LDS across chunks
   for (int i = tid; i < LQp * SS; i += 256) S[i] = 0.f;
   for (int e0 = 0; e0 < E; e0 += AC) {
+    const int ec = ((E - e0 < AC ? E - e0 : AC) + 3) & ~3;   // features of this chunk, padded to 4
     __syncthreads();
     for (int i = tid; i < LQp * AC; i += 256) {
       const int r = i / AC, c = i - r * AC;
@@ -273,8 +405,7 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
     for (int t = w; t < nqt * nkt; t += 4) {
       const int qt = t / nkt, kt = t - qt * nkt;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < AC; kk += 4) {
+      for (int kk = 0; kk < ec; kk += 4) {
         const float a = Qc[(16 * qt + (lane & 15)) * (AC + 1) + kk + (lane >> 4)];
         const float bb = Kc[(16 * kt + (lane & 15)) * (AC + 1) + kk + (lane >> 4)];
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
@@ -320,26 +451,32 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
     return op.O + (size_t)b * LQ * op.ldo + (size_t)h * LQ * E + (size_t)i * E;
   };
 
-  // ---- softmax rows of the selected queries (P written over S in place), one wave per row
-  for (int r = w; r < nsel; r += 4) {
-    const int q = sparse ? sel[r] : r;
+  // ---- softmax rows of the selected queries (P written over S in place): RL lanes per row, so a wave
+  //      takes 64 / RL rows at once (short rows: 16 lanes, 4 rows per wave pass)
+  const int RL = LK <= 32 ? 16 : 64, RPW = 64 / RL;
+  const int sub = lane / RL, ll = lane - sub * RL;
+  for (int r0 = w * RPW; r0 < nsel; r0 += 4 * RPW) {
+    const int r = r0 + sub;
+    const bool active = r < nsel;
+    const int q = active ? (sparse ? sel[r] : r) : 0;
     float* Srow = S + q * SS;
-    const int kmax = op.causal ? q + 1 : LK;   // keys j > q masked
+    const int kmax = !active ? 0 : (op.causal ? q + 1 : LK);   // keys j > q masked
     float mx = -INFINITY;
-    for (int j = lane; j < kmax; j += 64) mx = fmaxf(mx, Srow[j] * scale);
-    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    for (int j = ll; j < kmax; j += RL) mx = fmaxf(mx, Srow[j] * scale);
+    for (int o = RL / 2; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     float sum = 0.f;
-    for (int j = lane; j < LK; j += 64) {
+    const int kend = active ? LK : 0;
+    for (int j = ll; j < kend; j += RL) {
       const float p = j < kmax ? expf(Srow[j] * scale - mx) : 0.f;
       Srow[j] = p;
       sum += p;
     }
-    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    for (int o = RL / 2; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
     const float inv = 1.0f / sum;
-    for (int j = lane; j < LK; j += 64) Srow[j] *= inv;
-    if (op.attns) {
+    for (int j = ll; j < kend; j += RL) Srow[j] *= inv;
+    if (op.attns && active) {
       float* A = op.attns + (size_t)b * op.attn_bstride + ((size_t)h * LQ + q) * LK;
-      for (int j = lane; j < LK; j += 64) A[j] = Srow[j];
+      for (int j = ll; j < LK; j += RL) A[j] = Srow[j];
     }
   }
   if (sparse && op.attns) {
@@ -351,6 +488,7 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
   //      O = P·V for the selected rows on the f32 MFMA (16 selected rows × 16 features per tile)
   const int nrt = (nsel + 15) / 16;
   for (int e0 = 0; e0 < E; e0 += AC) {
+    const int nct = ((E - e0 < AC ? E - e0 : AC) + 15) / 16;   // 16-feature output tiles of this chunk
     __syncthreads();   // P complete (first chunk) / the previous chunk's V no longer read
     for (int i = tid; i < LKp * AC; i += 256) {
       const int r = i / AC, c = i - r * AC;
@@ -373,8 +511,8 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
         }
       }
     }
-    for (int t = w; t < nrt * (AC / 16); t += 4) {
-      const int rt = t / (AC / 16), et = t - rt * (AC / 16);
+    for (int t = w; t < nrt * nct; t += 4) {
+      const int rt = t / nct, et = t - rt * nct;
       const int rs = 16 * rt + (lane & 15);
       const int qa = sparse ? sel[rs < nsel ? rs : nsel - 1] : (rs < nsel ? rs : nsel - 1);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -402,7 +540,8 @@ size_t attn_lds_bytes(int LQ, int LK) {
 // ---------------------------------------------------------------------------------- launchers
 int launch_gemm(const GemmOp& op, hipStream_t st) {
   if (op.M <= 0 || op.N <= 0) return 0;
-  if (op.M <= 1024) {   // few rows (batch-1 latency): more, shorter workgroups
+  if (op.ln_g && (op.N > GT || op.row_t0 > 0)) return -3;
+  if (op.M <= 1024 && !op.ln_g) {   // few rows (batch-1 latency): more, shorter workgroups
     hipLaunchKernelGGL(lw_gemm_s, dim3((op.M + SM - 1) / SM, (op.N + GT - 1) / GT), dim3(256), 0, st, op);
   } else {
     hipLaunchKernelGGL(lw_gemm, dim3((op.M + GT - 1) / GT, (op.N + GT - 1) / GT), dim3(256), 0, st, op);

@@ -3,6 +3,7 @@
 // shapes the fused kernels do not carry.  The model (weights as fp32 [N][K] matrices, the plan of
 // layers) is built by cet_api.cpp (build_lw); this file owns the device side.
 #include <algorithm>
+#include <functional>
 
 #include "cet_lw.h"
 
@@ -11,6 +12,7 @@ namespace lw {
 
 Model::~Model() {
   if (gexec) (void)hipGraphExecDestroy(gexec);
+  if (dexec) (void)hipGraphExecDestroy(dexec);
   if (cap) (void)hipStreamDestroy(cap);
   if (d_blob) (void)hipFree(d_blob);
   if (ws) (void)hipFree(ws);
@@ -51,6 +53,10 @@ int Model::ensure_ws(int B) {
     (void)hipGraphExecDestroy(gexec);
     gexec = nullptr;
   }
+  if (dexec) {
+    (void)hipGraphExecDestroy(dexec);
+    dexec = nullptr;
+  }
   if (ws && hipFree(ws) != hipSuccess) return -1;
   ws = nullptr;
   if (hipMalloc((void**)&ws, need * sizeof(float)) != hipSuccess) return -1;
@@ -60,12 +66,38 @@ int Model::ensure_ws(int B) {
 
 // The operator sequence is captured once per batch size into a hipGraph over fixed workspace
 // buffers; a forward then costs two input copies, one graph launch and one output copy on the
-// caller's stream instead of ≈110 kernel launches (batch-1 latency is launch-bound).  Forwards that
-// materialise attention maps launch the operators directly.
+// caller's stream instead of ≈110 kernel launches (batch-1 latency is launch-bound).  A caller that
+// repeats its buffers (a serving loop) gets a second graph captured over those buffers and skips the
+// copies.  Forwards that materialise attention maps launch the operators directly.
+static int capture(hipStream_t cap, hipGraphExec_t* exec, const std::function<int(hipStream_t)>& body) {
+  hipGraph_t g = nullptr;
+  // captured on a private stream (the caller's may be the null stream, which cannot capture); the
+  // instantiated graph is launched on the caller's stream
+  if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -1;
+  const int rc = body(cap);
+  if (hipStreamEndCapture(cap, &g) != hipSuccess || rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return -1;
+  }
+  const hipError_t ie = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  return ie == hipSuccess ? 0 : -1;
+}
+
 int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
                    hipStream_t st) {
   if (ensure_ws(B)) return -1;
   if (attns && out_attn) return enqueue(x_enc, x_dec, B, out, attns, idx_dev, st);
+  const Key key{x_enc, x_dec, out, idx_dev, B};
+  if (!(dexec && dkey == key) && last == key) {
+    if (dexec) (void)hipGraphExecDestroy(dexec);
+    dexec = nullptr;
+    if (capture(cap, &dexec, [&](hipStream_t s) { return enqueue(x_enc, x_dec, B, out, nullptr, idx_dev, s); }))
+      return -1;
+    dkey = key;
+  }
+  last = key;
+  if (dexec && dkey == key) return hipGraphLaunch(dexec, st) == hipSuccess ? 0 : -1;
   const size_t nXE = (size_t)B * L0 * C, nXDi = (size_t)B * Ld * Cd, nOUT = (size_t)B * pred * c_out;
   float* XE = ws + ws_floats(B) - 64 - nOUT - nXDi - nXE;
   float* XDi = XE + nXE;
@@ -75,18 +107,8 @@ int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, fl
   if (!gexec || gB != B) {
     if (gexec) (void)hipGraphExecDestroy(gexec);
     gexec = nullptr;
-    hipGraph_t g = nullptr;
-    // captured on a private stream (the caller's may be the null stream, which cannot capture); the
-    // instantiated graph is launched on the caller's stream
-    if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -1;
-    const int rc = enqueue(XE, XDi, B, OUTb, nullptr, idx_dev, cap);
-    if (hipStreamEndCapture(cap, &g) != hipSuccess || rc) {
-      if (g) (void)hipGraphDestroy(g);
+    if (capture(cap, &gexec, [&](hipStream_t s) { return enqueue(XE, XDi, B, OUTb, nullptr, idx_dev, s); }))
       return -1;
-    }
-    const hipError_t ie = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (ie != hipSuccess) return -1;
     gB = B;
   }
   if (hipGraphLaunch(gexec, st) != hipSuccess) return -1;
@@ -125,6 +147,18 @@ int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, fl
     LnOp o{M, D, L, Lo, off, Xi, Yo, P + g, P + b};
     if (!rc) rc = launch_layernorm(o, st);
   };
+  // a residual GEMM whose in-place LayerNorm follows: fused into its epilogue when one 64-wide tile holds
+  // whole rows (d_model ≤ 64), else the separate LayerNorm launch
+  auto run_ln = [&](GemmOp g, int L, size_t lg, size_t lb) {
+    if (D <= 64) {
+      g.ln_g = P + lg;
+      g.ln_b = P + lb;
+      run(g);
+    } else {
+      run(g);
+      ln(g.Y, g.Y, g.M, L, L, 0, lg, lb);
+    }
+  };
   auto attend = [&](const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv, float* O, int LQ,
                     int LK, int prob_, int causal, int mix_, int call, float* amap) {
     AttnOp a{};
@@ -154,20 +188,18 @@ int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, fl
       attend(QKV, 3 * HE, QKV + HE, 3 * HE, QKV + 2 * HE, 3 * HE, CTX, L, L, prob, 0, 0, ly.call,
              attns && out_attn ? attns + ly.attn_off : nullptr);
       {
-        GemmOp g = gemm(CTX, M, D, HE, HE, ly.wo, ly.bo, X, D, L);   // x + new_x (encoder.py:49)
+        GemmOp g = gemm(CTX, M, D, HE, HE, ly.wo, ly.bo, X, D, L);   // x = norm1(x + new_x) (encoder.py:49)
         g.R = X; g.ldr = D;
-        run(g);
+        run_ln(g, L, ly.g1, ly.be1);
       }
-      ln(X, X, M, L, L, 0, ly.g1, ly.be1);
       {
         GemmOp g = gemm(X, M, dff, D, D, ly.w1, ly.b1, HID, dff, L);
         g.act = act;
         run(g);
-        GemmOp g2 = gemm(HID, M, D, dff, dff, ly.w2, ly.b2, X, D, L);
+        GemmOp g2 = gemm(HID, M, D, dff, dff, ly.w2, ly.b2, X, D, L);   // norm2(x + y)
         g2.R = X; g2.ldr = D;
-        run(g2);
+        run_ln(g2, L, ly.g2, ly.be2);
       }
-      ln(X, X, M, L, L, 0, ly.g2, ly.be2);
       if (ly.conv) {   // ConvLayer (encoder.py:22-28)
         GemmOp g = gemm(X, M, D, 3 * D, D, ly.wc, ly.sh, HID, D, L);
         g.amode = 1; g.Cin = D; g.scale = P + ly.sc; g.act = 3;
@@ -190,29 +222,26 @@ int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, fl
     run(gemm(XD, Md, 3 * HE, D, D, ly.wqkv, ly.bqkv, QKV, 3 * HE, Ld));
     attend(QKV, 3 * HE, QKV + HE, 3 * HE, QKV + 2 * HE, 3 * HE, CTX, Ld, Ld, prob, 1, mix, ly.call, nullptr);
     {
-      GemmOp g = gemm(CTX, Md, D, HE, HE, ly.wo, ly.bo, XD, D, Ld);
+      GemmOp g = gemm(CTX, Md, D, HE, HE, ly.wo, ly.bo, XD, D, Ld);   // norm1(x + self-attention)
       g.R = XD; g.ldr = D;
-      run(g);
+      run_ln(g, Ld, ly.g1, ly.be1);
     }
-    ln(XD, XD, Md, Ld, Ld, 0, ly.g1, ly.be1);
     run(gemm(XD, Md, HE, D, D, ly.wcq, ly.bcq, QC, HE, Ld));
     run(gemm(ENC, B * S, 2 * HE, D, D, ly.wckv, ly.bckv, QKV, 2 * HE, S));
     attend(QC, HE, QKV, 2 * HE, QKV + HE, 2 * HE, CTX, Ld, S, 0, 0, 0, -1, nullptr);
     {
-      GemmOp g = gemm(CTX, Md, D, HE, HE, ly.wco, ly.bco, XD, D, Ld);
+      GemmOp g = gemm(CTX, Md, D, HE, HE, ly.wco, ly.bco, XD, D, Ld);   // norm2(x + cross-attention)
       g.R = XD; g.ldr = D;
-      run(g);
+      run_ln(g, Ld, ly.g2, ly.be2);
     }
-    ln(XD, XD, Md, Ld, Ld, 0, ly.g2, ly.be2);
     {
       GemmOp g = gemm(XD, Md, dff, D, D, ly.w1, ly.b1, HID, dff, Ld);
       g.act = act;
       run(g);
-      GemmOp g2 = gemm(HID, Md, D, dff, dff, ly.w2, ly.b2, XD, D, Ld);
+      GemmOp g2 = gemm(HID, Md, D, dff, dff, ly.w2, ly.b2, XD, D, Ld);   // norm3(x + y)
       g2.R = XD; g2.ldr = D;
-      run(g2);
+      run_ln(g2, Ld, ly.g3, ly.be3);
     }
-    ln(XD, XD, Md, Ld, Ld, 0, ly.g3, ly.be3);
   }
   ln(XD, XD, Md, Ld, Ld, 0, dnorm_g, dnorm_b);
   {
