@@ -107,6 +107,8 @@ def cpu_baseline(batch: int = 512, reps: int = 5):
             "sample": f"median of {reps} forwards at B={batch} ({t_big * 1e3:.0f} ms each) of the reference's torch "
                       f"CPU forward (oracle/informer_torch.py, float32, eval/no_grad, {threads} threads)",
             "b1_seq_per_s": round(1.0 / t_one, 1), "cpu_model": host["model"],
+            "cores_note": "threads = min(physical cores, usable logical CPUs, OMP_NUM_THREADS): a one-GPU job on "
+                          "the 8-GPU box is given 16 CPUs (OMP_NUM_THREADS=16), this GPU's share of the host",
             "host_physical_cores": host["physical_cores"], "host_usable_logical": host["usable_logical"]}
 
 

@@ -409,6 +409,7 @@ struct Packer {
     d.scale = scale ? vec(scale, N, Np) : NONE;
     return d;
   }
+#ifdef CET_FP8_SCALED
   // An LSQ integer grid q ∈ [−128, 127] for the block-scaled fp8 MFMA (v4 P_FP8, cet_v4.hpp): per
   // 64-feature block kb, byte j = 8b + i of the lane's 32 carries feature 64·kb + 32·(b&1) + 8(lane>>4) + i
   // as hi = ⌊q/16⌋ (bytes 0-15, the MFMA's scale blocks 0-1, ×2^4) or lo = q mod 16 (bytes 16-31, blocks
@@ -440,6 +441,33 @@ struct Packer {
     d.scale = scale ? vec(scale, N, Np) : NONE;
     return d;
   }
+#else
+  // An LSQ integer grid q ∈ [−128, 127] as e4m3 pairs (v4 P_FP8, default form): lane fragment = 8 bytes
+  // of 16·⌊q/16⌋ then 8 bytes of q mod 16, both exact in e4m3; same 16 B per lane per k-step as bf16.
+  GemmDesc gemm_fp8(const std::vector<float>& q, int N, int K, const float* bias, const float* scale) {
+    GemmDesc d{};
+    const int Np = r16(N), Kp = r32(K);
+    d.w = (uint32_t)(wb.size() / 8);
+    d.n = (uint16_t)Np;
+    d.k = (uint16_t)Kp;
+    for (int nt = 0; nt < Np / 16; ++nt)
+      for (int ks = 0; ks < Kp / 32; ++ks)
+        for (int lane = 0; lane < 64; ++lane) {
+          uint8_t by[16];
+          for (int j = 0; j < 8; ++j) {
+            const int n = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
+            const int v = n < N && k < K ? (int)q[(size_t)n * K + k] : 0;
+            const int hi = (int)std::floor(v / 16.0);
+            by[j] = f2e4m3((float)(16 * hi));
+            by[8 + j] = f2e4m3((float)(v - 16 * hi));
+          }
+          for (int j = 0; j < 8; ++j) wb.push_back((uint16_t)(by[2 * j] | (by[2 * j + 1] << 8)));
+        }
+    d.bias = bias ? vec(bias, N, Np) : NONE;
+    d.scale = scale ? vec(scale, N, Np) : NONE;
+    return d;
+  }
+#endif
   uint32_t vec(const float* v, int n, int npad) {
     while (pb.size() % 4) pb.push_back(0.f);
     const uint32_t off = (uint32_t)pb.size();

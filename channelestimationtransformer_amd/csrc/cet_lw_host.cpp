@@ -28,6 +28,10 @@ size_t Model::push(const std::vector<float>& v) {
 
 int Model::upload() {
   if (blob.size() > d_blob_n) {
+    // the captured graphs hold the old blob's address: drop them with it
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (dexec) (void)hipGraphExecDestroy(dexec);
+    gexec = dexec = nullptr;
     if (d_blob && hipFree(d_blob) != hipSuccess) return -1;
     d_blob = nullptr;
     if (hipMalloc((void**)&d_blob, blob.size() * sizeof(float)) != hipSuccess) return -1;
