@@ -66,6 +66,8 @@ struct AttnOp {
 };
 
 int launch_gemm(const GemmOp& op, hipStream_t st);
+// the FFN pair in one launch (d_model, d_ff ≤ 64): g1 = conv1 + activation, g2 = conv2 + residual (+ LayerNorm)
+int launch_ffn(const GemmOp& g1, const GemmOp& g2, hipStream_t st);
 int launch_layernorm(const LnOp& op, hipStream_t st);
 int launch_maxpool(const float* X, float* Y, int B, int L, int Lo, int D, hipStream_t st);
 int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStream_t st);

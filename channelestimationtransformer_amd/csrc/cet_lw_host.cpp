@@ -153,6 +153,19 @@ int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, fl
   };
   // a residual GEMM whose in-place LayerNorm follows: fused into its epilogue when one 64-wide tile holds
   // whole rows (d_model ≤ 64), else the separate LayerNorm launch
+  // the FFN pair (conv1 + activation, conv2 + residual + LayerNorm): one launch with the hidden rows in
+  // LDS when d_model and d_ff ≤ 64, else two GEMMs
+  auto run_ffn = [&](const GemmOp& g1, GemmOp g2, int L, size_t lg, size_t lb) {
+    if (D <= 64 && dff <= 64) {
+      g2.ln_g = P + lg;
+      g2.ln_b = P + lb;
+      if (!rc) rc = launch_ffn(g1, g2, st);
+    } else {
+      run(g1);
+      run(g2);
+      ln(g2.Y, g2.Y, g2.M, L, L, 0, lg, lb);
+    }
+  };
   auto run_ln = [&](GemmOp g, int L, size_t lg, size_t lb) {
     if (D <= 64) {
       g.ln_g = P + lg;
@@ -199,10 +212,9 @@ int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, fl
       {
         GemmOp g = gemm(X, M, dff, D, D, ly.w1, ly.b1, HID, dff, L);
         g.act = act;
-        run(g);
         GemmOp g2 = gemm(HID, M, D, dff, dff, ly.w2, ly.b2, X, D, L);   // norm2(x + y)
         g2.R = X; g2.ldr = D;
-        run_ln(g2, L, ly.g2, ly.be2);
+        run_ffn(g, g2, L, ly.g2, ly.be2);
       }
       if (ly.conv) {   // ConvLayer (encoder.py:22-28)
         GemmOp g = gemm(X, M, D, 3 * D, D, ly.wc, ly.sh, HID, D, L);
@@ -241,10 +253,9 @@ int Model::enqueue(const float* x_enc, const float* x_dec, int B, float* out, fl
     {
       GemmOp g = gemm(XD, Md, dff, D, D, ly.w1, ly.b1, HID, dff, Ld);
       g.act = act;
-      run(g);
       GemmOp g2 = gemm(HID, Md, D, dff, dff, ly.w2, ly.b2, XD, D, Ld);   // norm3(x + y)
       g2.R = XD; g2.ldr = D;
-      run_ln(g2, Ld, ly.g3, ly.be3);
+      run_ffn(g, g2, Ld, ly.g3, ly.be3);
     }
   }
   ln(XD, XD, Md, Ld, Ld, 0, dnorm_g, dnorm_b);
