@@ -594,154 +594,6 @@ __global__ void __launch_bounds__(256) lw_attention(AttnOp op) {
   }
 }
 
-// Short sequences and heads (LQ, LK, E ≤ 32: the d_model-64 checkpoint, E = 8, L ≤ 25): one wave per
-// (sequence, head), four per 256-thread workgroup, each in its own LDS region — no workgroup barriers,
-// every hand-off between lanes is wave-local.  Same operator sequence as lw_attention.
-constexpr int SA = 32, SAS = SA + 1;                        // rows / row stride (floats) of the regions
-constexpr int SA_FLOATS = 3 * SA * SAS + 3 * SA;            // S | Q | K (then V) | M | sel | flag
-__device__ __forceinline__ void wave_sync() {   // this wave's LDS ops complete and stay ordered
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-__global__ void __launch_bounds__(256) lw_attention_small(AttnOp op, int n_pairs) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int p = blockIdx.x * 4 + w;
-  if (p >= n_pairs) return;   // wave-uniform; nothing below synchronises the workgroup
-  float* S = sm + w * SA_FLOATS;                   // [SA][SAS]
-  float* Qc = S + SA * SAS;                        // [SA][SAS]
-  float* Kc = Qc + SA * SAS;                       // [SA][SAS], later V
-  float* Mv = Kc + SA * SAS;                       // [SA]
-  int* sel = reinterpret_cast<int*>(Mv + SA);      // [SA]
-  int* flag = sel + SA;                            // [SA]
-  const int LQ = op.LQ, LK = op.LK, E = op.E;
-  const int b = p / op.H, h = p - (p / op.H) * op.H;
-  const float* Qg = op.Q + (size_t)b * LQ * op.ldq + (size_t)h * E;
-  const float* Kg = op.K + (size_t)b * LK * op.ldk + (size_t)h * E;
-  const float* Vg = op.V + (size_t)b * LK * op.ldv + (size_t)h * E;
-  const int nqt = (LQ + 15) >> 4, nkt = (LK + 15) >> 4, Ep = (E + 3) & ~3;
-  for (int i = lane; i < SA * SA; i += 64) {
-    const int r = i >> 5, c = i & 31;
-    Qc[r * SAS + c] = r < LQ && c < E ? Qg[(size_t)r * op.ldq + c] : 0.f;
-    Kc[r * SAS + c] = r < LK && c < E ? Kg[(size_t)r * op.ldk + c] : 0.f;
-  }
-  wave_sync();
-  // ---- S = Q·Kᵀ (f32 MFMA), tile by tile
-  for (int qt = 0; qt < nqt; ++qt)
-    for (int kt = 0; kt < nkt; ++kt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int kk = 0; kk < Ep; kk += 4)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Qc[(16 * qt + (lane & 15)) * SAS + kk + (lane >> 4)],
-                                                  Kc[(16 * kt + (lane & 15)) * SAS + kk + (lane >> 4)], acc, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) S[(16 * qt + 4 * (lane >> 4) + r) * SAS + 16 * kt + (lane & 15)] = acc[r];
-    }
-  wave_sync();
-  const bool sparse = op.prob && op.u < LQ;
-  if (sparse) {
-    // ProbSparse M per query from its sampled keys (attn.py:89-105), then the top-u by rank
-    if (lane < LQ) {
-      const int32_t* ix = op.idx + (size_t)lane * op.U;
-      float mx = -INFINITY, sum = 0.f;
-      for (int j = 0; j < op.U; ++j) {
-        const float sv = S[lane * SAS + ix[j]];
-        mx = fmaxf(mx, sv);
-        sum += sv;
-      }
-      Mv[lane] = mx - sum / (float)LK;
-    }
-    wave_sync();
-    if (lane < LQ) {
-      const float m = Mv[lane];
-      int rank = 0;
-      for (int j = 0; j < LQ; ++j) {
-        const float o = Mv[j];
-        rank += (o > m) || (o == m && j < lane);
-      }
-      flag[lane] = rank < op.u;
-      if (rank < op.u) sel[rank] = lane;
-    }
-    wave_sync();
-  }
-  const int nsel = sparse ? op.u : LQ;
-  const float scale = 1.0f / sqrtf((float)E);
-  auto ctx_ptr = [&](int i) -> float* {
-    if (!op.mix) return op.O + ((size_t)b * LQ + i) * op.ldo + (size_t)h * E;
-    return op.O + (size_t)b * LQ * op.ldo + (size_t)h * LQ * E + (size_t)i * E;
-  };
-  // ---- softmax rows of the selected queries, 16 lanes per row (LK ≤ 32), P over S in place
-  {
-    const int sub = lane >> 4, ll = lane & 15;
-    for (int r0 = 0; r0 < nsel; r0 += 4) {
-      const int r = r0 + sub;
-      const bool active = r < nsel;
-      const int q = active ? (sparse ? sel[r] : r) : 0;
-      float* Srow = S + q * SAS;
-      const int kmax = !active ? 0 : (op.causal ? q + 1 : LK);
-      float mx = -INFINITY;
-      for (int j = ll; j < kmax; j += 16) mx = fmaxf(mx, Srow[j] * scale);
-      for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-      float sum = 0.f;
-      const int kend = active ? LK : 0;
-      for (int j = ll; j < kend; j += 16) {
-        const float pv = j < kmax ? expf(Srow[j] * scale - mx) : 0.f;
-        Srow[j] = pv;
-        sum += pv;
-      }
-      for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
-      const float inv = 1.0f / sum;
-      for (int j = ll; j < kend; j += 16) Srow[j] *= inv;
-      if (op.attns && active) {
-        float* A = op.attns + (size_t)b * op.attn_bstride + ((size_t)h * LQ + q) * LK;
-        for (int j = ll; j < LK; j += 16) A[j] = Srow[j];
-      }
-    }
-  }
-  if (sparse && op.attns) {
-    float* A = op.attns + (size_t)b * op.attn_bstride + (size_t)h * LQ * LK;
-    for (int i = lane; i < LQ * LK; i += 64)
-      if (!flag[i / LK]) A[i] = 1.0f / (float)LK;
-  }
-  // ---- V into the K region, the unselected rows' initial context, O = P·V for the selected rows
-  for (int i = lane; i < SA * SA; i += 64) {
-    const int r = i >> 5, c = i & 31;
-    Kc[r * SAS + c] = r < LK && c < E ? Vg[(size_t)r * op.ldv + c] : 0.f;
-  }
-  wave_sync();
-  if (sparse && lane < E) {
-    const int e = lane;
-    if (!op.causal) {   // mean over keys (attn.py:116-119)
-      float sv = 0.f;
-      for (int j = 0; j < LK; ++j) sv += Kc[j * SAS + e];
-      const float mean = sv / (float)LK;
-      for (int q = 0; q < LQ; ++q)
-        if (!flag[q]) ctx_ptr(q)[e] = mean;
-    } else {            // cumsum over keys (attn.py:120-125)
-      float sv = 0.f;
-      for (int q = 0; q < LQ; ++q) {
-        sv += Kc[q * SAS + e];
-        if (!flag[q]) ctx_ptr(q)[e] = sv;
-      }
-    }
-  }
-  const int nrt = (nsel + 15) >> 4, nct = (E + 15) >> 4, LKp = nkt * 16;
-  for (int rt = 0; rt < nrt; ++rt)
-    for (int et = 0; et < nct; ++et) {
-      const int rs = 16 * rt + (lane & 15);
-      const int qa = sparse ? sel[rs < nsel ? rs : nsel - 1] : (rs < nsel ? rs : nsel - 1);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < LKp; k0 += 4)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(S[qa * SAS + k0 + (lane >> 4)],
-                                                  Kc[(k0 + (lane >> 4)) * SAS + 16 * et + (lane & 15)], acc, 0, 0, 0);
-      const int e = 16 * et + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = 16 * rt + 4 * (lane >> 4) + r;
-        if (rr < nsel && e < E) ctx_ptr(sparse ? sel[rr] : rr)[e] = acc[r];
-      }
-    }
-}
-
 size_t attn_lds_bytes(int LQ, int LK) {
   const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15;
   return sizeof(float) * ((size_t)LQp * (LKp + 1) + (size_t)LQp * (AC + 1) + (size_t)LKp * (AC + 1) + LQp) +
@@ -782,19 +634,11 @@ int launch_window(const float* X, float* Y, int B, int L0, int L, int D, hipStre
 }
 int prepare_attention() {
   // once per (device, kernel), thread-safe (cet_api.cpp)
-  return cet::ensure_lds_attr(reinterpret_cast<const void*>(lw_attention)) &&
-                 cet::ensure_lds_attr(reinterpret_cast<const void*>(lw_attention_small))
-             ? 0
-             : -1;
+  return cet::ensure_lds_attr(reinterpret_cast<const void*>(lw_attention)) ? 0 : -1;
 }
 int launch_attention(const AttnOp& op, int B, hipStream_t st) {
   if (op.LQ > LW_LMAX || op.LK > LW_LMAX) return -3;
   if (prepare_attention()) return -1;
-  if (op.LQ <= SA && op.LK <= SA && op.E <= SA) {
-    const int n = B * op.H;
-    hipLaunchKernelGGL(lw_attention_small, dim3((n + 3) / 4), dim3(256), 4 * SA_FLOATS * sizeof(float), st, op, n);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-  }
   hipLaunchKernelGGL(lw_attention, dim3(B * op.H), dim3(256), attn_lds_bytes(op.LQ, op.LK), st, op);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
