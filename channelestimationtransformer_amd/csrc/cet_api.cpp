@@ -1555,6 +1555,7 @@ static int forward_lw(cet_engine* e, const float* x_enc, const float* x_dec, int
   const int tk = timing_mark(e, st);
   const int rc = e->lw->forward(x_enc, x_dec, B, out, attns, e->lw->d_idx, st);
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
+  e->last_path = e->lw->last_fused ? CET_PATH_LW_FUSED : CET_PATH_LW;
   if (rc) return fail(CET_E_HIP, std::string("layer-wise launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (label && cet_launch_nmse_split(out, label, B, e->icfg.out_len, e->icfg.c_out, nmse_acc, nullptr, 1, nmse_sums, st))
     return fail(CET_E_HIP, "nmse launch failed");

@@ -75,6 +75,48 @@ int launch_attention(const AttnOp& op, int B, hipStream_t st);
 size_t attn_lds_bytes(int LQ, int LK);
 int prepare_attention();   // dynamic-LDS attribute of lw_attention (before any capture)
 
+// ------------------------------------------------------------- fused form (cet_lwf.hip)
+// The whole forward of one sequence in one 256-thread workgroup with every activation in LDS, for
+// models whose per-sequence working set fits (the d_model-64 MimoSimulation checkpoint: 77 KB, two
+// workgroups per CU).  Same operators and arithmetic class as the layer-wise launches (fp32 operands on
+// v_mfma_f32_16x16x4_f32); weights pre-packed in MFMA fragment order so every weight load of a wave is
+// one coalesced 1 KB read: Wp[nt][kq][lane][j] = W[16nt + (lane & 15)][16kq + 4j + (lane >> 4)].
+constexpr uint32_t FNONE = 0xffffffffu;
+constexpr int F_MAX_ENC = 4, F_MAX_EL = 8, F_MAX_DEC = 4, F_MAX_CALLS = F_MAX_ENC * F_MAX_EL + F_MAX_DEC;
+constexpr int F_LMAX = 128;   // rows per sequence (8 m-tiles)
+struct FG {
+  uint32_t w;      // packed weight (float offset into the packed blob)
+  uint32_t b, s;   // bias / scale (float offsets into the model blob) or FNONE
+  int N, K;
+};
+struct FEnc {
+  FG qkv, o, f1, f2, cv;
+  uint32_t g1, b1, g2, b2;
+  int conv, Lo, call;
+};
+struct FDec {
+  FG qkv, o, cq, ckv, co, f1, f2;
+  uint32_t g1, b1, g2, b2, g3, b3;
+  int call;
+};
+struct FPlan {
+  int C, Cd, c_out, L0, Ld, pred, D, H, E, HE, dff, S, prob, mix, act, stack, nenc, ndec;
+  int nl[F_MAX_ENC], eL0[F_MAX_ENC], eoff[F_MAX_ENC];
+  uint32_t ng[F_MAX_ENC], nb[F_MAX_ENC];
+  FG emb_e, emb_d, proj;
+  uint32_t pe_e, pe_d, dng, dnb;
+  int call_U[F_MAX_CALLS], call_u[F_MAX_CALLS];
+  uint32_t call_off[F_MAX_CALLS];
+  // LDS layout (float offsets) and row strides
+  int oE0, oX, oT, oCTX, oENC, oXD, oSCR, scr_floats, lds_floats;
+  int ldD, ldT, ldH, ldF, ldKV, ldIN, ldINd;
+  FEnc enc[F_MAX_ENC][F_MAX_EL];
+  FDec dec[F_MAX_DEC];
+};
+int launch_fused(const FPlan* d_plan, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
+                 const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st);
+int prepare_fused();
+
 // ------------------------------------------------------------------ host model (cet_lw_host.cpp)
 // Weights as fp32 [N][K] matrices in one device blob (float offsets below); ProbSparse draws of a
 // forward concatenated in call order (call c's [LQ][U] table at idx_off[c]).
@@ -124,6 +166,15 @@ struct Model {
   hipGraphExec_t dexec = nullptr;
   Key dkey{}, last{};
   hipStream_t cap = nullptr;        // capture stream
+  // fused form (cet_lwf.hip): the plan, the packed weights; chosen for every forward without attention
+  // maps when the per-sequence working set fits one workgroup's LDS (CET_LW_FUSED=0 turns it off)
+  FPlan fplan{};
+  bool fused_ok = false, use_fused = true, last_fused = false;
+  size_t fused_lds = 0;
+  std::vector<float> pblob;
+  FPlan* d_fplan = nullptr;
+  float* d_pblob = nullptr;
+  int build_fused();
   ~Model();
   size_t ws_floats(int B) const;
   int ensure_ws(int B);

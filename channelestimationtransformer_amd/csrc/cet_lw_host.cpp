@@ -3,6 +3,9 @@
 // shapes the fused kernels do not carry.  The model (weights as fp32 [N][K] matrices, the plan of
 // layers) is built by cet_api.cpp (build_lw); this file owns the device side.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <functional>
 
 #include "cet_lw.h"
@@ -17,6 +20,8 @@ Model::~Model() {
   if (d_blob) (void)hipFree(d_blob);
   if (ws) (void)hipFree(ws);
   if (d_idx) (void)hipFree(d_idx);
+  if (d_fplan) (void)hipFree(d_fplan);
+  if (d_pblob) (void)hipFree(d_pblob);
 }
 
 size_t Model::push(const std::vector<float>& v) {
@@ -40,7 +45,115 @@ int Model::upload() {
   if (hipMemcpy(d_blob, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (!d_idx && idx_total && hipMalloc((void**)&d_idx, idx_total * sizeof(int32_t)) != hipSuccess) return -1;
   if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) return -1;
+  if (build_fused()) return -1;
   return prepare_attention() ? -1 : 0;
+}
+
+// The fused form's plan (cet_lw.h FPlan) and packed weights, rebuilt with every upload.  fused_ok stays
+// false when the sequence's working set does not fit one workgroup's LDS (or a count exceeds the plan).
+int Model::build_fused() {
+  fused_ok = false;
+  const char* env = std::getenv("CET_LW_FUSED");
+  use_fused = !(env && std::strcmp(env, "0") == 0);
+  const int nenc = (int)enc.size(), ndec = (int)dec.size();
+  const int Lm = std::max(L0, Ld);
+  const bool why = std::getenv("CET_LW_FUSED_WHY") != nullptr;
+  if (why) fprintf(stderr, "lw fused: nenc %d ndec %d calls %zu Lm %d S %d\n", nenc, ndec, call_u.size(), Lm, S);
+  if (nenc < 1 || nenc > F_MAX_ENC || ndec > F_MAX_DEC || (int)call_u.size() > F_MAX_CALLS) return 0;
+  if (Lm > F_LMAX || S > F_LMAX || S < 1) return 0;
+  for (const auto& e : enc)
+    if ((int)e.size() > F_MAX_EL) return 0;
+  auto r16 = [](int x) { return (x + 15) & ~15; };
+  auto pad = [](int w) { return ((w + 31) & ~31) + 2; };   // ≡ 2 mod 32 floats
+  FPlan& p = fplan;
+  std::memset(&p, 0, sizeof(p));
+  p.C = C; p.Cd = Cd; p.c_out = c_out; p.L0 = L0; p.Ld = Ld; p.pred = pred; p.D = D; p.H = H; p.E = E; p.HE = HE;
+  p.dff = dff; p.S = S; p.prob = prob; p.mix = mix; p.act = act; p.stack = stack; p.nenc = nenc; p.ndec = ndec;
+  p.ldD = pad(D); p.ldT = pad(3 * HE); p.ldH = pad(HE); p.ldF = pad(std::max(dff, D)); p.ldKV = pad(2 * HE);
+  p.ldIN = C | 1; p.ldINd = Cd | 1;
+  const size_t nE0 = stack ? (size_t)r16(L0) * p.ldD : 0, nX = (size_t)r16(L0) * p.ldD;
+  const size_t nT = std::max({(size_t)r16(Lm) * p.ldT, (size_t)r16(Ld) * p.ldH + (size_t)r16(S) * p.ldKV,
+                              (size_t)r16(Lm) * p.ldF, (size_t)r16(L0) * p.ldIN, (size_t)r16(Ld) * p.ldINd});
+  const size_t nCTX = (size_t)r16(Lm) * p.ldH, nENC = (size_t)r16(S) * p.ldD, nXD = (size_t)r16(Ld) * p.ldD;
+  auto scr_of = [&](int LQ, int LK) { return (size_t)r16(LQ) * (r16(LK) + 1) + 3 * (size_t)r16(LQ); };
+  size_t scr = std::max({scr_of(L0, L0), scr_of(Ld, Ld), scr_of(Ld, S)});
+  scr = (scr + 3) & ~(size_t)3;
+  size_t o = 0;
+  auto place = [&](size_t n) {
+    const size_t at = o;
+    o += (n + 3) & ~(size_t)3;
+    return (int)at;
+  };
+  p.oE0 = place(nE0); p.oX = place(nX); p.oT = place(nT); p.oCTX = place(nCTX); p.oENC = place(nENC);
+  p.oXD = place(nXD); p.oSCR = place(4 * scr);
+  p.scr_floats = (int)scr;
+  p.lds_floats = (int)o;
+  fused_lds = o * sizeof(float);
+  if (why) fprintf(stderr, "lw fused: lds %zu bytes\n", fused_lds);
+  if (fused_lds > 160 * 1024) return 0;
+  // packed weights: Wp[nt][kq][lane][j] = W[16nt + (lane & 15)][16kq + 4j + (lane >> 4)]
+  pblob.clear();
+  auto pack = [&](size_t w, int N, int K, size_t bias, size_t scale) {
+    const int NT = (N + 15) / 16, KQ = (K + 15) / 16;
+    const size_t at = pblob.size();
+    pblob.resize(at + (size_t)NT * KQ * 256, 0.f);
+    for (int nt = 0; nt < NT; ++nt)
+      for (int kq = 0; kq < KQ; ++kq)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 4; ++j) {
+            const int n = 16 * nt + (lane & 15), k = 16 * kq + 4 * j + (lane >> 4);
+            if (n < N && k < K) pblob[at + (((size_t)nt * KQ + kq) * 64 + lane) * 4 + j] = blob[w + (size_t)n * K + k];
+          }
+    FG g;
+    g.w = (uint32_t)at; g.b = (uint32_t)bias; g.s = scale == (size_t)-1 ? FNONE : (uint32_t)scale; g.N = N; g.K = K;
+    return g;
+  };
+  const size_t none = (size_t)-1;
+  p.emb_e = pack(emb_enc_w, D, 3 * C, emb_enc_b, none);
+  p.emb_d = pack(emb_dec_w, D, 3 * Cd, emb_dec_b, none);
+  p.proj = pack(proj_w, c_out, D, proj_b, none);
+  p.pe_e = (uint32_t)pe_enc; p.pe_d = (uint32_t)pe_dec; p.dng = (uint32_t)dnorm_g; p.dnb = (uint32_t)dnorm_b;
+  for (int i = 0; i < nenc; ++i) {
+    p.nl[i] = (int)enc[i].size(); p.eL0[i] = enc_L0[i]; p.eoff[i] = enc_off[i];
+    p.ng[i] = (uint32_t)norm_g[i]; p.nb[i] = (uint32_t)norm_b[i];
+    for (int l = 0; l < p.nl[i]; ++l) {
+      const EncLayer& s = enc[i][l];
+      FEnc& f = p.enc[i][l];
+      f.qkv = pack(s.wqkv, 3 * HE, D, s.bqkv, none);
+      f.o = pack(s.wo, D, HE, s.bo, none);
+      f.f1 = pack(s.w1, dff, D, s.b1, none);
+      f.f2 = pack(s.w2, D, dff, s.b2, none);
+      if (s.conv) f.cv = pack(s.wc, D, 3 * D, s.sh, s.sc);
+      f.g1 = (uint32_t)s.g1; f.b1 = (uint32_t)s.be1; f.g2 = (uint32_t)s.g2; f.b2 = (uint32_t)s.be2;
+      f.conv = s.conv; f.Lo = s.L_out; f.call = s.call;
+    }
+  }
+  for (int l = 0; l < ndec; ++l) {
+    const DecLayer& s = dec[l];
+    FDec& f = p.dec[l];
+    f.qkv = pack(s.wqkv, 3 * HE, D, s.bqkv, none);
+    f.o = pack(s.wo, D, HE, s.bo, none);
+    f.cq = pack(s.wcq, HE, D, s.bcq, none);
+    f.ckv = pack(s.wckv, 2 * HE, D, s.bckv, none);
+    f.co = pack(s.wco, D, HE, s.bco, none);
+    f.f1 = pack(s.w1, dff, D, s.b1, none);
+    f.f2 = pack(s.w2, D, dff, s.b2, none);
+    f.g1 = (uint32_t)s.g1; f.b1 = (uint32_t)s.be1; f.g2 = (uint32_t)s.g2; f.b2 = (uint32_t)s.be2;
+    f.g3 = (uint32_t)s.g3; f.b3 = (uint32_t)s.be3; f.call = s.call;
+  }
+  for (size_t c = 0; c < call_u.size(); ++c) {
+    p.call_U[c] = call_U[c]; p.call_u[c] = call_u[c]; p.call_off[c] = (uint32_t)idx_off[c];
+  }
+  if (blob.size() >= FNONE || pblob.size() >= FNONE) return 0;
+  if (!d_fplan && hipMalloc((void**)&d_fplan, sizeof(FPlan)) != hipSuccess) return -1;
+  if (d_pblob) (void)hipFree(d_pblob);
+  d_pblob = nullptr;
+  if (hipMalloc((void**)&d_pblob, pblob.size() * sizeof(float)) != hipSuccess) return -1;
+  if (hipMemcpy(d_pblob, pblob.data(), pblob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (hipMemcpy(d_fplan, &p, sizeof(FPlan), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (prepare_fused()) return -1;
+  fused_ok = true;
+  return 0;
 }
 
 size_t Model::ws_floats(int B) const {
@@ -90,6 +203,9 @@ static int capture(hipStream_t cap, hipGraphExec_t* exec, const std::function<in
 
 int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
                    hipStream_t st) {
+  // the fused form: one launch, no workspace, no staging copies
+  last_fused = fused_ok && use_fused && !(attns && out_attn);
+  if (last_fused) return launch_fused(d_fplan, fused_lds, d_blob, d_pblob, x_enc, x_dec, out, idx_dev, B, st);
   if (ensure_ws(B)) return -1;
   if (attns && out_attn) return enqueue(x_enc, x_dec, B, out, attns, idx_dev, st);
   const Key key{x_enc, x_dec, out, idx_dev, B};

@@ -1,0 +1,424 @@
+// Fused layer-wise forward (cet_lw.h FPlan): the InformerStack / Informer forward of one sequence per
+// 256-thread workgroup, every activation resident in LDS, for models whose per-sequence working set fits
+// (the MimoSimulation checkpoint architecture: d_model 64, seq_len 25, e_layers [4,3]).  It runs the same
+// operator sequence as the layer-wise launches (cet_lw_host.cpp Model::enqueue) in one launch:
+//   DataEmbedding (embed.py:118-135)              circular k=3 conv GEMM + pe rows
+//   EncoderStack windows (encoder.py:95-106)      x[:, -L:] copies, Encoder.norm into the concatenation
+//   EncoderLayer (encoder.py:31-56)               Q/K/V GEMM, attention, O GEMM + residual, LN, FFN, LN
+//   ConvLayer (encoder.py:6-28)                   circular conv GEMM with folded BN, ELU, MaxPool(3,2,1)
+//   DecoderLayer (decoder.py:6-41)                causal self-attention (+ mix), cross-attention, FFN
+//   projection (model.py:264)                     the last pred_len rows straight to HBM
+//   ProbAttention / FullAttention (attn.py:37-175) per (head, wave) with the call's draws from HBM
+// Arithmetic class: fp32 operands on v_mfma_f32_16x16x4_f32, as the layer-wise engine.
+//
+// Layout: wave w computes the 16-column n-tiles w, w + 4, … of a GEMM over every m-tile of the sequence
+// (one weight fragment feeds up to 8 m-tiles); its weights are a coalesced f32x4 per lane per 16 k
+// (host-packed, FPlan comment), the A operand is read from the LDS image; LDS row strides are ≡ 2 mod 32
+// floats (lanes 0-15 and 16-31 of an A read hit 32 distinct banks).  Attention: wave w owns heads w,
+// w + 4, …; scores, ProbSparse M, rank top-u and P live in the wave's own LDS scratch, no workgroup
+// barrier inside.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cet_device.hpp"
+#include "cet_lw.h"
+
+namespace cet {
+bool ensure_lds_attr(const void* kern);   // cet_api.cpp
+}
+
+namespace cet {
+namespace lw {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int FMT = F_LMAX / 16;   // m-tiles per sequence
+constexpr int KW = 4;              // k-quads (16 k each) of weights per register window
+
+__device__ __forceinline__ float fgelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float act_of(float y, int act) {
+  if (act == 1) return fgelu(y);
+  if (act == 2) return fmaxf(y, 0.f);
+  if (act == 3) return y > 0.f ? y : expm1f(y);
+  return y;
+}
+
+// Y[t][n] = act(Σ_k A(t, k)·W[n][k] · scale[n] + bias[n] + pe[t][n]) (+ Y[t][n] if res), t < L, n < N.
+// amode 0: A(t, k) = A[t·lda + k]; amode 1: circular k=3 conv, A(t, tap·Cin + c) = A[((t − 1 + tap) mod L)·lda + c].
+// gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in HBM instead of Y.
+__device__ __noinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
+                                   const float* A, int lda, int amode, int Cin, int L, float* Y, int ldy,
+                                   const float* __restrict__ pe, int act, bool res, float* __restrict__ gout = nullptr,
+                                   int t0 = 0, int ldo = 0) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int NT = (g.N + 15) >> 4, KQ = (g.K + 15) >> 4, MT = (L + 15) >> 4;
+  const float* bias = g.b != FNONE ? blob + g.b : nullptr;
+  const float* scale = g.s != FNONE ? blob + g.s : nullptr;
+  for (int nt = w; nt < NT; nt += 4) {
+    f32x4 acc[FMT];
+#pragma unroll
+    for (int m = 0; m < FMT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4* wp = reinterpret_cast<const f32x4*>(pw + g.w) + (size_t)nt * KQ * 64 + lane;
+    // weights of KW k-quads in registers, the next window's loads in flight during this window's MFMAs
+    f32x4 wa[KW], wb[KW];
+#pragma unroll
+    for (int i = 0; i < KW; ++i) wa[i] = i < KQ ? wp[(size_t)i * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < KQ; kc += KW) {
+#pragma unroll
+      for (int i = 0; i < KW; ++i) wb[i] = kc + KW + i < KQ ? wp[(size_t)(kc + KW + i) * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < KW; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = 16 * (kc + i) + 4 * j + q4;
+          const bool kv = k < g.K;
+          int tap = 0, c = k;
+          if (amode) {
+            tap = (k >= Cin) + (k >= 2 * Cin);
+            c = k - tap * Cin;
+          }
+#pragma unroll
+          for (int m = 0; m < FMT; ++m) {
+            if (m >= MT) break;
+            int t = 16 * m + r16;
+            if (amode) {
+              t = t < L ? t : L - 1;
+              int r = t - 1 + tap;
+              r = r < 0 ? r + L : (r >= L ? r - L : r);
+              t = r;
+            }
+            const float a = kv ? A[t * lda + c] : 0.f;
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wa[i][j], acc[m], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < KW; ++i) wa[i] = wb[i];
+    }
+    // epilogue: lane holds rows 16m + 4·q4 + r, column n
+    const int n = 16 * nt + r16;
+    if (n >= g.N) continue;
+    const float sc = scale ? scale[n] : 1.f;
+    const float bi = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int m = 0; m < FMT; ++m) {
+      if (m >= MT) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * m + 4 * q4 + r;
+        if (t >= L) continue;
+        float y = acc[m][r] * sc + bi;
+        if (pe) y += pe[t * g.N + n];
+        y = act_of(y, act);
+        if (res) y += Y[t * ldy + n];
+        if (gout) {
+          if (t >= t0) gout[(t - t0) * ldo + n] = y;
+        } else {
+          Y[t * ldy + n] = y;
+        }
+      }
+    }
+  }
+}
+
+// LayerNorm of L rows of width D (eps 1e-5, biased variance; encoder.py:49-56), one wave per row, the
+// reduction order of lw_layernorm; Y may alias X.
+__device__ __noinline__ void fln(const float* X, int ldx, int L, int D, const float* __restrict__ g,
+                                    const float* __restrict__ bb, float* Y, int ldy) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int t = w; t < L; t += 4) {
+    const float* x = X + t * ldx;
+    float s = 0.f;
+    for (int c = lane; c < D; c += 64) s += x[c];
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)D;
+    float q = 0.f;
+    for (int c = lane; c < D; c += 64) {
+      const float d = x[c] - mean;
+      q = fmaf(d, d, q);
+    }
+    for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float inv = 1.0f / sqrtf(q / (float)D + 1e-5f);
+    float* y = Y + t * ldy;
+    for (int c = lane; c < D; c += 64) y[c] = (x[c] - mean) * inv * g[c] + bb[c];
+  }
+}
+
+// Attention of one sequence (attn.py:37-175; the semantics of lw_attention): wave w takes heads w, w + 4, …
+// Q rows i at column h·E (stride ldq), K/V rows j; sparse: ProbSparse with the call's draws ix[LQ][U] and u;
+// causal: keys j > i masked (cumsum(V) as the initial context); mix: the (L, H, E) → (H, L, E) re-view of the
+// output (O dense [LQ][HE] at stride ldo).
+__device__ __noinline__ void fattn(const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv,
+                                      float* O, int ldo, int H, int E, int LQ, int LK, int causal, int mix,
+                                      int sparse, int U, int u, const int32_t* __restrict__ ix, float* scr) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15, SS = LKp + 1;
+  const int HE = H * E;
+  float* S = scr;
+  float* Mv = S + LQp * SS;
+  int* sel = reinterpret_cast<int*>(Mv + LQp);
+  int* flag = sel + LQp;
+  const float scale = 1.0f / sqrtf((float)E);
+  const int nqt = LQp >> 4, nkt = LKp >> 4, Ep = (E + 3) & ~3;
+  for (int h = w; h < H; h += 4) {
+    const int hc = h * E;
+    auto store = [&](int q, int e, float v) {
+      if (!mix) {
+        O[q * ldo + hc + e] = v;
+      } else {
+        const int f = h * LQ * E + q * E + e, row = f / HE;
+        O[row * ldo + (f - row * HE)] = v;
+      }
+    };
+    // ---- S = Q_h · K_hᵀ (unscaled)
+    for (int tt = 0; tt < nqt * nkt; ++tt) {
+      const int qt = tt / nkt, kt = tt - qt * nkt;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk < Ep; kk += 4) {
+        const int e = kk + q4;
+        const float a = e < E ? Q[(16 * qt + r16) * ldq + hc + e] : 0.f;
+        const float b = e < E ? K[(16 * kt + r16) * ldk + hc + e] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[(16 * qt + 4 * q4 + r) * SS + 16 * kt + r16] = acc[r];
+    }
+    wave_lds_sync();
+    // ---- ProbSparse: M per query from its sampled keys (sum over L_K), exact top-u by rank
+    if (sparse) {
+      for (int q = lane; q < LQ; q += 64) {
+        const int32_t* iq = ix + q * U;
+        float mx = -INFINITY, sum = 0.f;
+        for (int j = 0; j < U; ++j) {
+          const float s = S[q * SS + iq[j]];
+          mx = fmaxf(mx, s);
+          sum += s;
+        }
+        Mv[q] = mx - sum / (float)LK;
+      }
+      wave_lds_sync();
+      for (int q = lane; q < LQ; q += 64) {
+        const float m = Mv[q];
+        int rank = 0;
+        for (int j = 0; j < LQ; ++j) {
+          const float o = Mv[j];
+          rank += (o > m) || (o == m && j < q);
+        }
+        flag[q] = rank < u;
+        if (rank < u) sel[rank] = q;
+      }
+      wave_lds_sync();
+    }
+    const int nsel = sparse ? u : LQ;
+    // ---- softmax(scale · S) of the selected rows, P over S (zero beyond the row's last key)
+    for (int r = lane; r < nsel; r += 64) {
+      const int q = sparse ? sel[r] : r;
+      float* row = S + q * SS;
+      const int kmax = causal ? q + 1 : LK;
+      float mx = -INFINITY;
+      for (int j = 0; j < kmax; ++j) mx = fmaxf(mx, row[j] * scale);
+      float sum = 0.f;
+      for (int j = 0; j < LKp; ++j) {
+        const float p = j < kmax ? expf(row[j] * scale - mx) : 0.f;
+        row[j] = p;
+        sum += p;
+      }
+      const float inv = 1.0f / sum;
+      for (int j = 0; j < kmax; ++j) row[j] *= inv;
+    }
+    wave_lds_sync();
+    // ---- the initial context of the unselected rows: mean(V) (attn.py:116-119) or cumsum(V) (:120-125)
+    if (sparse) {
+      for (int e = lane; e < E; e += 64) {
+        float sv = 0.f;
+        if (!causal) {
+          for (int j = 0; j < LK; ++j) sv += V[j * ldv + hc + e];
+          const float mean = sv / (float)LK;
+          for (int q = 0; q < LQ; ++q)
+            if (!flag[q]) store(q, e, mean);
+        } else {
+          for (int q = 0; q < LQ; ++q) {
+            sv += V[q * ldv + hc + e];
+            if (!flag[q]) store(q, e, sv);
+          }
+        }
+      }
+    }
+    // ---- O = P · V for the selected rows (16 rows × 16 features per tile)
+    const int nrt = (nsel + 15) >> 4, nct = (E + 15) >> 4;
+    for (int tt = 0; tt < nrt * nct; ++tt) {
+      const int rt = tt / nct, et = tt - rt * nct;
+      const int rs = 16 * rt + r16;
+      const int rc = rs < nsel ? rs : nsel - 1;
+      const int qa = sparse ? sel[rc] : rc;
+      const int e = 16 * et + r16;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < LKp; k0 += 4) {
+        const float a = S[qa * SS + k0 + q4];
+        const float b = e < E ? V[(k0 + q4) * ldv + hc + e] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 16 * rt + 4 * q4 + r;
+        if (rr < nsel && e < E) store(sparse ? sel[rr] : rr, e, acc[r]);
+      }
+    }
+    wave_lds_sync();   // S / sel of this head read before the next head's scores overwrite them
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lw_fused(const FPlan* __restrict__ p, const float* __restrict__ blob,
+                                                const float* __restrict__ pw, const float* __restrict__ x_enc,
+                                                const float* __restrict__ x_dec, float* __restrict__ out,
+                                                const int32_t* __restrict__ idx) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int D = p->D, H = p->H, E = p->E, HE = p->HE, L0 = p->L0, Ld = p->Ld;
+  const int ldD = p->ldD, ldT = p->ldT, ldH = p->ldH, ldF = p->ldF, ldKV = p->ldKV;
+  float* E0 = sm + p->oE0;
+  float* X = sm + p->oX;
+  float* T = sm + p->oT;
+  float* CTX = sm + p->oCTX;
+  float* ENC = sm + p->oENC;
+  float* XD = sm + p->oXD;
+  float* scr = sm + p->oSCR + w * p->scr_floats;
+  // zero LDS (padded rows and columns stay finite: they only ever meet zero weights or masked keys), then
+  // stage this sequence's encoder input rows
+  for (int i = tid; i < p->lds_floats; i += 256) sm[i] = 0.f;
+  __syncthreads();
+  {
+    const int C = p->C, ldIN = p->ldIN;
+    const float* xe = x_enc + (size_t)b * L0 * C;
+    for (int i = tid; i < L0 * C; i += 256) {
+      const int t = i / C;
+      T[t * ldIN + (i - t * C)] = xe[i];
+    }
+  }
+  __syncthreads();
+  // ---- DataEmbedding of the encoder input
+  fgemm(blob, pw, p->emb_e, T, p->ldIN, 1, p->C, L0, p->stack ? E0 : X, ldD, blob + p->pe_e, 0, false);
+  __syncthreads();
+  // ---- encoders
+  for (int i = 0; i < p->nenc; ++i) {
+    int L = p->eL0[i];
+    if (p->stack) {   // x[:, -L:] of the embedded input
+      for (int k = tid; k < L * D; k += 256) {
+        const int t = k / D, c = k - t * D;
+        X[t * ldD + c] = E0[(L0 - L + t) * ldD + c];
+      }
+      __syncthreads();
+    }
+    for (int l = 0; l < p->nl[i]; ++l) {
+      const FEnc* ly = &p->enc[i][l];
+      fgemm(blob, pw, ly->qkv, X, ldD, 0, 0, L, T, ldT, nullptr, 0, false);
+      __syncthreads();
+      {
+        const int call = ly->call;
+        const int u = call >= 0 ? p->call_u[call] : L;
+        const int sparse = p->prob && call >= 0 && u < L;
+        fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
+              u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
+      }
+      __syncthreads();
+      fgemm(blob, pw, ly->o, CTX, ldH, 0, 0, L, X, ldD, nullptr, 0, true);   // x + attention (encoder.py:44-49)
+      __syncthreads();
+      fln(X, ldD, L, D, blob + ly->g1, blob + ly->b1, X, ldD);
+      __syncthreads();
+      fgemm(blob, pw, ly->f1, X, ldD, 0, 0, L, T, ldF, nullptr, p->act, false);
+      __syncthreads();
+      fgemm(blob, pw, ly->f2, T, ldF, 0, 0, L, X, ldD, nullptr, 0, true);
+      __syncthreads();
+      fln(X, ldD, L, D, blob + ly->g2, blob + ly->b2, X, ldD);
+      __syncthreads();
+      if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
+        fgemm(blob, pw, ly->cv, X, ldD, 1, D, L, T, ldF, nullptr, 3, false);
+        __syncthreads();
+        const int Lo = ly->Lo;
+        for (int k = tid; k < Lo * D; k += 256) {
+          const int t = k / D, c = k - t * D;
+          float v = T[(2 * t) * ldF + c];
+          if (2 * t + 1 < L) v = fmaxf(v, T[(2 * t + 1) * ldF + c]);
+          if (2 * t - 1 >= 0) v = fmaxf(v, T[(2 * t - 1) * ldF + c]);
+          X[t * ldD + c] = v;
+        }
+        __syncthreads();
+        L = Lo;
+      }
+    }
+    // Encoder.norm → rows [eoff, eoff + L) of the concatenated stack output
+    fln(X, ldD, L, D, blob + p->ng[i], blob + p->nb[i], ENC + p->eoff[i] * ldD, ldD);
+    __syncthreads();
+  }
+  // ---- decoder
+  {
+    const int Cd = p->Cd, ldIN = p->ldINd;
+    const float* xd = x_dec + (size_t)b * Ld * Cd;
+    for (int i = tid; i < Ld * Cd; i += 256) {
+      const int t = i / Cd;
+      T[t * ldIN + (i - t * Cd)] = xd[i];
+    }
+  }
+  __syncthreads();
+  fgemm(blob, pw, p->emb_d, T, p->ldINd, 1, p->Cd, Ld, XD, ldD, blob + p->pe_d, 0, false);
+  __syncthreads();
+  const int S = p->S;
+  float* QC = T;
+  float* KV = T + ((Ld + 15) & ~15) * ldH;
+  for (int l = 0; l < p->ndec; ++l) {
+    const FDec* ly = &p->dec[l];
+    fgemm(blob, pw, ly->qkv, XD, ldD, 0, 0, Ld, T, ldT, nullptr, 0, false);
+    __syncthreads();
+    {
+      const int call = ly->call;
+      const int u = call >= 0 ? p->call_u[call] : Ld;
+      const int sparse = p->prob && call >= 0 && u < Ld;
+      fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
+            call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
+    }
+    __syncthreads();
+    fgemm(blob, pw, ly->o, CTX, ldH, 0, 0, Ld, XD, ldD, nullptr, 0, true);   // norm1(x + self-attention)
+    __syncthreads();
+    fln(XD, ldD, Ld, D, blob + ly->g1, blob + ly->b1, XD, ldD);
+    __syncthreads();
+    fgemm(blob, pw, ly->cq, XD, ldD, 0, 0, Ld, QC, ldH, nullptr, 0, false);
+    fgemm(blob, pw, ly->ckv, ENC, ldD, 0, 0, S, KV, ldKV, nullptr, 0, false);
+    __syncthreads();
+    fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr);
+    __syncthreads();
+    fgemm(blob, pw, ly->co, CTX, ldH, 0, 0, Ld, XD, ldD, nullptr, 0, true);   // norm2(x + cross-attention)
+    __syncthreads();
+    fln(XD, ldD, Ld, D, blob + ly->g2, blob + ly->b2, XD, ldD);
+    __syncthreads();
+    fgemm(blob, pw, ly->f1, XD, ldD, 0, 0, Ld, T, ldF, nullptr, p->act, false);
+    __syncthreads();
+    fgemm(blob, pw, ly->f2, T, ldF, 0, 0, Ld, XD, ldD, nullptr, 0, true);   // norm3(x + y)
+    __syncthreads();
+    fln(XD, ldD, Ld, D, blob + ly->g3, blob + ly->b3, XD, ldD);
+    __syncthreads();
+  }
+  fln(XD, ldD, Ld, D, blob + p->dng, blob + p->dnb, XD, ldD);
+  __syncthreads();
+  // projection of the last pred_len rows → out[b][pred][c_out]
+  fgemm(blob, pw, p->proj, XD, ldD, 0, 0, Ld, nullptr, 0, nullptr, 0, false,
+        out + (size_t)b * p->pred * p->c_out, Ld - p->pred, p->c_out);
+}
+
+int prepare_fused() {
+  return cet::ensure_lds_attr(reinterpret_cast<const void*>(lw_fused)) ? 0 : -1;
+}
+
+int launch_fused(const FPlan* d_plan, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
+                 const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (prepare_fused()) return -1;
+  hipLaunchKernelGGL(lw_fused, dim3(B), dim3(256), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // namespace lw
+}  // namespace cet

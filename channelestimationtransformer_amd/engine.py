@@ -189,10 +189,11 @@ class Engine:
         outputs)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
 
-    PATHS = {0: None, 4: "v4", 5: "v5", 41: "v4-split"}
+    PATHS = {0: None, 3: "layerwise", 4: "v4", 5: "v5", 31: "layerwise-fused", 41: "v4-split"}
 
     def last_path(self):
-        """The fused kernel the last Informer forward launched: "v5", "v4", "v4-split" or None."""
+        """The kernel path the last Informer forward took: "v5", "v4", "v4-split", "layerwise" (operator
+        launches), "layerwise-fused" (the layer-wise forward in one launch) or None."""
         return self.PATHS[check(lib.cet_last_path(self._h), "cet_last_path")]
 
     PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3}

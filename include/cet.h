@@ -127,9 +127,11 @@ int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
  * batches below n to generation 4.  Transformer engines have generation 4 only.  Generations 1-3 are
  * retired: CET_E_INVALID. */
 int cet_set_variant(cet_engine* e, int variant);
-/* The fused kernel the engine's last Informer forward launched: CET_PATH_V5, CET_PATH_V4,
- * CET_PATH_V4_SPLIT (v4 with the stack's encoders on separate workgroups), 0 before any. */
-enum { CET_PATH_V4 = 4, CET_PATH_V5 = 5, CET_PATH_V4_SPLIT = 41 };
+/* The kernel path the engine's last Informer forward took: CET_PATH_V5, CET_PATH_V4,
+ * CET_PATH_V4_SPLIT (v4 with the stack's encoders on separate workgroups), CET_PATH_LW (layer-wise
+ * operator launches), CET_PATH_LW_FUSED (the layer-wise forward fused into one launch, one workgroup
+ * per sequence with its activations in LDS), 0 before any. */
+enum { CET_PATH_LW = 3, CET_PATH_V4 = 4, CET_PATH_V5 = 5, CET_PATH_LW_FUSED = 31, CET_PATH_V4_SPLIT = 41 };
 int cet_last_path(cet_engine* e);
 
 /* Operand precision of the v4 kernel's dense layers (Informer engines):

@@ -65,6 +65,10 @@ CASES = {
     # (d_keys = d_model // n_heads, TrainInformer.py:236-264), d_ff and d_model beyond 128, and a
     # long, genuinely sparse decoder (label_len 25 + pred_len 9)
     "informer_d64_e43": dict(model="informer_stack", cfg=dict(d_model=64, e_layers=[4, 3]), B=2, acts=True),
+    # the MimoSimulation checkpoint's own architecture (Predict.py:91-93: seq_len 25, d_model 64, e_layers
+    # [4,3], attn "full"): the shape the fused layer-wise form carries
+    "informer_d64_s25_full": dict(model="informer_stack", cfg=dict(d_model=64, e_layers=[4, 3], seq_len=25,
+                                                                   attn="full"), B=2, acts=True),
     "informer_h5_ff256": dict(model="informer_stack", cfg=dict(n_heads=5, d_ff=256), B=2, acts=False),
     "informer_d256_h3_lab25": dict(model="informer_stack",
                                    cfg=dict(d_model=256, n_heads=3, d_ff=128, seq_len=48, label_len=25, pred_len=9),

@@ -171,3 +171,92 @@ def test_layerwise_serving_loop_graph_over_caller_buffers():
         np.testing.assert_array_equal(o.cpu().numpy(), ref)
     orc, _ = oracle_for(case).forward(xe_np, xd_np, case.idx)
     assert rel_nmse(ref, orc) < TOL
+
+
+
+CKPT = "informer_d64_s25_full"   # the MimoSimulation checkpoint architecture (Predict.py:91-93)
+
+
+def _random_batch(cfg, B, seed):
+    rng = np.random.default_rng(seed)
+    xe = rng.standard_normal((B, cfg["seq_len"], cfg["enc_in"])).astype(np.float32)
+    xd = rng.standard_normal((B, cfg["label_len"] + cfg["pred_len"], cfg["dec_in"])).astype(np.float32)
+    return xe, xd
+
+
+@pytest.mark.parametrize("B", [37, 512])
+def test_fused_layerwise_checkpoint_fixture_and_oracle(B):
+    """The checkpoint architecture (d_model 64, seq_len 25, e_layers [4,3], attn "full") runs on the fused
+    layer-wise form (one workgroup per sequence, every activation in LDS): the fixture's inputs against
+    the reference's own output, a random batch against the float64 oracle (a 64-row slice), and a
+    repeated forward bit for bit."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case(CKPT)
+    m = model_for(case)
+    eng = m.engine(torch.device("cuda:0"))
+    out, _, _ = run_engine(m, case.z["x_enc"], case.z["x_dec"], case.idx)
+    assert eng.last_path() == "layerwise-fused"
+    assert rel_nmse(out, case.z["out"]) < TOL, rel_nmse(out, case.z["out"])
+    xe, xd = _random_batch(case.cfg, B, 100 + B)
+    out, _, _ = run_engine(m, xe, xd, case.idx)
+    again, _, _ = run_engine(m, xe, xd, case.idx)
+    assert eng.last_path() == "layerwise-fused"
+    np.testing.assert_array_equal(out, again)
+    n = min(B, 64)
+    ref, _ = oracle_for(case).forward(xe[:n], xd[:n], case.idx)
+    assert rel_nmse(out[:n], ref) < TOL, rel_nmse(out[:n], ref)
+
+
+def test_fused_layerwise_equals_operator_launches():
+    """The fused form and the operator-launch form of one model agree at fp32 rounding level (same
+    arithmetic class; the softmax and P·V sums run in another order); a forward that materialises the
+    attention maps keeps the operator launches."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case(CKPT)
+    xe, xd = _random_batch(case.cfg, 96, 5)
+    m = model_for(case)
+    fused, _, _ = run_engine(m, xe, xd, case.idx)
+    assert m.engine(torch.device("cuda:0")).last_path() == "layerwise-fused"
+    os.environ["CET_LW_FUSED"] = "0"
+    try:
+        m2 = model_for(case)
+        eng2 = m2.engine(torch.device("cuda:0"))
+    finally:
+        del os.environ["CET_LW_FUSED"]
+    ops, _, _ = run_engine(m2, xe, xd, case.idx)
+    assert eng2.last_path() == "layerwise"
+    assert rel_nmse(fused, ops) < 1e-11, rel_nmse(fused, ops)
+    run_engine(m, case.z["x_enc"], case.z["x_dec"], case.idx, attns=True)
+    assert m.engine(torch.device("cuda:0")).last_path() == "layerwise"
+
+
+@pytest.mark.parametrize("B", [3, 256])
+def test_fused_layerwise_probsparse_vs_oracle(B):
+    """The same architecture with attn "prob" (attn.py:73-175): the first encoder layer is genuinely
+    sparse (u = 5·ceil(ln 25) = 20 of 25 queries: rank top-u, mean(V) rows), the decoder self-attention
+    causal with mix; explicit draws, fused form against the float64 oracle at fp32 level."""
+    _gpu()
+    import dataclasses
+
+    from engine_util import model_for, run_engine
+
+    from channelestimationtransformer_amd.rng import draw_indices
+    from oracle.informer_np import sample_shapes
+
+    base = load_case(CKPT)
+    meta = dict(base.meta)
+    meta["cfg"] = dict(base.cfg, attn="prob")
+    case = dataclasses.replace(base, meta=meta)
+    orc = oracle_for(case)
+    idx = draw_indices(sample_shapes(orc.cfg), seed=9)
+    m = model_for(case)
+    xe, xd = _random_batch(case.cfg, B, 7 + B)
+    out, _, _ = run_engine(m, xe, xd, idx)
+    assert m.engine(torch.device("cuda:0")).last_path() == "layerwise-fused"
+    n = min(B, 64)
+    ref, _ = orc.forward(xe[:n], xd[:n], idx)
+    assert rel_nmse(out[:n], ref) < TOL, rel_nmse(out[:n], ref)
