@@ -44,19 +44,49 @@ __device__ __forceinline__ float act_of(float y, int act) {
   return y;
 }
 
+extern __shared__ __attribute__((aligned(16))) float lsm[];   // the workgroup's LDS (dynamic size)
+
+// Sum over the 64 lanes, every lane gets it: quad permutes, row half-mirror and mirror (DPP), then the
+// 16- and 32-lane swaps (gfx950 v_permlane16/32_swap) — VALU only, no LDS round trip.
+__device__ __forceinline__ float dpp_f(float v, int ctrl) {
+  switch (ctrl) {
+    case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+    case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+    case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  }
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f(v, 0xB1);    // quad_perm [1,0,3,2]
+  v += dpp_f(v, 0x4E);    // quad_perm [2,3,0,1]
+  v += dpp_f(v, 0x141);   // row_half_mirror: lane i of 8 with lane 7 − i
+  v += dpp_f(v, 0x140);   // row_mirror: lane i of 16 with lane 15 − i
+  v = swap_pair_sum16(v);
+  return swap_pair_sum32(v);
+}
+
+// A value every lane holds the same copy of, made provably uniform (scalar registers, scalar branches)
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // Y[t][n] = act(Σ_k A(t, k)·W[n][k] · scale[n] + bias[n] + pe[t][n]) (+ Y[t][n] if res), t < L, n < N.
-// amode 0: A(t, k) = A[t·lda + k]; amode 1: circular k=3 conv, A(t, tap·Cin + c) = A[((t − 1 + tap) mod L)·lda + c].
-// gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in HBM instead of Y.
+// A and Y are LDS float offsets.  AMODE 0: A(t, k) = A[t·lda + k]; AMODE 1: circular k=3 conv,
+// A(t, tap·Cin + c) = A[((t − 1 + tap) mod L)·lda + c].  gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in
+// HBM instead of Y.
+template <int AMODE>
 __device__ __noinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
-                                   const float* A, int lda, int amode, int Cin, int L, float* Y, int ldy,
-                                   const float* __restrict__ pe, int act, bool res, float* __restrict__ gout = nullptr,
-                                   int t0 = 0, int ldo = 0) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+                                   int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
+                                   int act, int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   const int r16 = lane & 15, q4 = lane >> 4;
-  const int NT = (g.N + 15) >> 4, KQ = (g.K + 15) >> 4, MT = (L + 15) >> 4;
-  const float* bias = g.b != FNONE ? blob + g.b : nullptr;
-  const float* scale = g.s != FNONE ? blob + g.s : nullptr;
+  const int N = uni(g.N), K = uni(g.K);
+  A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
+  const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4, MT = (L + 15) >> 4;
+  const bool has_b = uni(g.b) != (int)FNONE, has_s = uni(g.s) != (int)FNONE;
   for (int nt = w; nt < NT; nt += 4) {
+    const int n = 16 * nt + r16;
+    // epilogue vectors requested before the K loop (their latency hides under the MFMAs)
+    const float sc = has_s && n < N ? blob[g.s + n] : 1.f;
+    const float bi = has_b && n < N ? blob[g.b + n] : 0.f;
     f32x4 acc[FMT];
 #pragma unroll
     for (int m = 0; m < FMT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -73,24 +103,25 @@ __device__ __noinline__ void fgemm(const float* __restrict__ blob, const float* 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int k = 16 * (kc + i) + 4 * j + q4;
-          const bool kv = k < g.K;
+          const bool kv = k < K;
           int tap = 0, c = k;
-          if (amode) {
+          if (AMODE) {
             tap = (k >= Cin) + (k >= 2 * Cin);
             c = k - tap * Cin;
           }
 #pragma unroll
           for (int m = 0; m < FMT; ++m) {
-            if (m >= MT) break;
-            int t = 16 * m + r16;
-            if (amode) {
-              t = t < L ? t : L - 1;
-              int r = t - 1 + tap;
-              r = r < 0 ? r + L : (r >= L ? r - L : r);
-              t = r;
+            if (m < MT) {
+              int t = 16 * m + r16;
+              if (AMODE) {
+                t = t < L ? t : L - 1;
+                int r = t - 1 + tap;
+                r = r < 0 ? r + L : (r >= L ? r - L : r);
+                t = r;
+              }
+              const float a = kv ? lsm[A + t * lda + c] : 0.f;
+              acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wa[i][j], acc[m], 0, 0, 0);
             }
-            const float a = kv ? A[t * lda + c] : 0.f;
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wa[i][j], acc[m], 0, 0, 0);
           }
         }
       }
@@ -98,51 +129,48 @@ __device__ __noinline__ void fgemm(const float* __restrict__ blob, const float* 
       for (int i = 0; i < KW; ++i) wa[i] = wb[i];
     }
     // epilogue: lane holds rows 16m + 4·q4 + r, column n
-    const int n = 16 * nt + r16;
-    if (n >= g.N) continue;
-    const float sc = scale ? scale[n] : 1.f;
-    const float bi = bias ? bias[n] : 0.f;
+    if (n >= N) continue;
 #pragma unroll
     for (int m = 0; m < FMT; ++m) {
-      if (m >= MT) break;
+      if (m < MT) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = 16 * m + 4 * q4 + r;
-        if (t >= L) continue;
-        float y = acc[m][r] * sc + bi;
-        if (pe) y += pe[t * g.N + n];
-        y = act_of(y, act);
-        if (res) y += Y[t * ldy + n];
-        if (gout) {
-          if (t >= t0) gout[(t - t0) * ldo + n] = y;
-        } else {
-          Y[t * ldy + n] = y;
+        for (int r = 0; r < 4; ++r) {
+          const int t = 16 * m + 4 * q4 + r;
+          if (t >= L) continue;
+          float y = acc[m][r] * sc + bi;
+          if (pe) y += pe[t * N + n];
+          y = act_of(y, act);
+          if (res) y += lsm[Y + t * ldy + n];
+          if (gout) {
+            if (t >= t0) gout[(t - t0) * ldo + n] = y;
+          } else {
+            lsm[Y + t * ldy + n] = y;
+          }
         }
       }
     }
   }
 }
 
-// LayerNorm of L rows of width D (eps 1e-5, biased variance; encoder.py:49-56), one wave per row, the
-// reduction order of lw_layernorm; Y may alias X.
-__device__ __noinline__ void fln(const float* X, int ldx, int L, int D, const float* __restrict__ g,
-                                    const float* __restrict__ bb, float* Y, int ldy) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// LayerNorm of L rows of width D (eps 1e-5, biased variance; encoder.py:49-56), one wave per row; Y may
+// alias X.
+__device__ __noinline__ void fln(int X, int ldx, int L, int D, const float* __restrict__ g,
+                                 const float* __restrict__ bb, int Y, int ldy) {
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  X = uni(X); ldx = uni(ldx); L = uni(L); D = uni(D); Y = uni(Y); ldy = uni(ldy);
   for (int t = w; t < L; t += 4) {
-    const float* x = X + t * ldx;
+    const int x = X + t * ldx;
     float s = 0.f;
-    for (int c = lane; c < D; c += 64) s += x[c];
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    const float mean = s / (float)D;
+    for (int c = lane; c < D; c += 64) s += lsm[x + c];
+    const float mean = wave_sum(s) / (float)D;
     float q = 0.f;
     for (int c = lane; c < D; c += 64) {
-      const float d = x[c] - mean;
+      const float d = lsm[x + c] - mean;
       q = fmaf(d, d, q);
     }
-    for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
-    const float inv = 1.0f / sqrtf(q / (float)D + 1e-5f);
-    float* y = Y + t * ldy;
-    for (int c = lane; c < D; c += 64) y[c] = (x[c] - mean) * inv * g[c] + bb[c];
+    const float inv = 1.0f / sqrtf(wave_sum(q) / (float)D + 1e-5f);
+    const int y = Y + t * ldy;
+    for (int c = lane; c < D; c += 64) lsm[y + c] = (lsm[x + c] - mean) * inv * g[c] + bb[c];
   }
 }
 
@@ -150,10 +178,18 @@ __device__ __noinline__ void fln(const float* X, int ldx, int L, int D, const fl
 // Q rows i at column h·E (stride ldq), K/V rows j; sparse: ProbSparse with the call's draws ix[LQ][U] and u;
 // causal: keys j > i masked (cumsum(V) as the initial context); mix: the (L, H, E) → (H, L, E) re-view of the
 // output (O dense [LQ][HE] at stride ldo).
-__device__ __noinline__ void fattn(const float* Q, int ldq, const float* K, int ldk, const float* V, int ldv,
-                                      float* O, int ldo, int H, int E, int LQ, int LK, int causal, int mix,
-                                      int sparse, int U, int u, const int32_t* __restrict__ ix, float* scr) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+__device__ __noinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H, int E,
+                                   int LQ, int LK, int causal, int mix, int sparse, int U, int u,
+                                   const int32_t* __restrict__ ix, int scro) {
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  Qo = uni(Qo); ldq = uni(ldq); Ko = uni(Ko); ldk = uni(ldk); Vo = uni(Vo); ldv = uni(ldv); Oo = uni(Oo);
+  ldo = uni(ldo); H = uni(H); E = uni(E); LQ = uni(LQ); LK = uni(LK); causal = uni(causal); mix = uni(mix);
+  sparse = uni(sparse); U = uni(U); u = uni(u); scro = uni(scro);
+  const float* Q = lsm + Qo;
+  const float* K = lsm + Ko;
+  const float* V = lsm + Vo;
+  float* O = lsm + Oo;
+  float* scr = lsm + scro;
   const int r16 = lane & 15, q4 = lane >> 4;
   const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15, SS = LKp + 1;
   const int HE = H * E;
@@ -219,14 +255,17 @@ __device__ __noinline__ void fattn(const float* Q, int ldq, const float* K, int 
       float* row = S + q * SS;
       const int kmax = causal ? q + 1 : LK;
       float mx = -INFINITY;
+#pragma unroll 8
       for (int j = 0; j < kmax; ++j) mx = fmaxf(mx, row[j] * scale);
       float sum = 0.f;
+#pragma unroll 8
       for (int j = 0; j < LKp; ++j) {
         const float p = j < kmax ? expf(row[j] * scale - mx) : 0.f;
         row[j] = p;
         sum += p;
       }
       const float inv = 1.0f / sum;
+#pragma unroll 8
       for (int j = 0; j < kmax; ++j) row[j] *= inv;
     }
     wave_lds_sync();
@@ -271,52 +310,65 @@ __device__ __noinline__ void fattn(const float* Q, int ldq, const float* K, int 
   }
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lw_fused(const FPlan* __restrict__ p, const float* __restrict__ blob,
-                                                const float* __restrict__ pw, const float* __restrict__ x_enc,
-                                                const float* __restrict__ x_dec, float* __restrict__ out,
-                                                const int32_t* __restrict__ idx) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+#ifdef LWF_STAMPS
+// diagnostic build: cycles of workgroup 0 per category (0 GEMM, 1 attention, 2 LayerNorm, 3 other), printed
+#define LWF_ST_DECL uint64_t st_acc[4] = {0, 0, 0, 0}; uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define LWF_ST(cat) { const uint64_t now_ = __builtin_amdgcn_s_memtime(); st_acc[cat] += now_ - st_prev; st_prev = now_; }
+#define LWF_ST_END if (blockIdx.x == 0 && threadIdx.x == 0) printf("lwf stamps gemm %llu attn %llu ln %llu other %llu\n", \
+    (unsigned long long)st_acc[0], (unsigned long long)st_acc[1], (unsigned long long)st_acc[2], (unsigned long long)st_acc[3]);
+#else
+#define LWF_ST_DECL
+#define LWF_ST(cat)
+#define LWF_ST_END
+#endif
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lw_fused(
+    const FPlan* __restrict__ p, const float* __restrict__ blob, const float* __restrict__ pw,
+    const float* __restrict__ x_enc, const float* __restrict__ x_dec, float* __restrict__ out,
+    const int32_t* __restrict__ idx) {
   const int tid = threadIdx.x, w = tid >> 6;
   const int b = blockIdx.x;
+  LWF_ST_DECL
   const int D = p->D, H = p->H, E = p->E, HE = p->HE, L0 = p->L0, Ld = p->Ld;
   const int ldD = p->ldD, ldT = p->ldT, ldH = p->ldH, ldF = p->ldF, ldKV = p->ldKV;
-  float* E0 = sm + p->oE0;
-  float* X = sm + p->oX;
-  float* T = sm + p->oT;
-  float* CTX = sm + p->oCTX;
-  float* ENC = sm + p->oENC;
-  float* XD = sm + p->oXD;
-  float* scr = sm + p->oSCR + w * p->scr_floats;
+  // LDS regions (float offsets into lsm)
+  const int E0 = p->oE0, X = p->oX, T = p->oT, CTX = p->oCTX, ENC = p->oENC, XD = p->oXD;
+  const int scr = p->oSCR + w * p->scr_floats;
   // zero LDS (padded rows and columns stay finite: they only ever meet zero weights or masked keys), then
   // stage this sequence's encoder input rows
-  for (int i = tid; i < p->lds_floats; i += 256) sm[i] = 0.f;
+  for (int i = tid; i < p->lds_floats; i += 256) lsm[i] = 0.f;
   __syncthreads();
+  LWF_ST(3)
   {
     const int C = p->C, ldIN = p->ldIN;
     const float* xe = x_enc + (size_t)b * L0 * C;
     for (int i = tid; i < L0 * C; i += 256) {
       const int t = i / C;
-      T[t * ldIN + (i - t * C)] = xe[i];
+      lsm[T + t * ldIN + (i - t * C)] = xe[i];
     }
   }
   __syncthreads();
+  LWF_ST(3)
   // ---- DataEmbedding of the encoder input
-  fgemm(blob, pw, p->emb_e, T, p->ldIN, 1, p->C, L0, p->stack ? E0 : X, ldD, blob + p->pe_e, 0, false);
+  fgemm<1>(blob, pw, p->emb_e, T, p->ldIN, p->C, L0, p->stack ? E0 : X, ldD, blob + p->pe_e, 0, 0);
   __syncthreads();
+  LWF_ST(0)
   // ---- encoders
   for (int i = 0; i < p->nenc; ++i) {
     int L = p->eL0[i];
     if (p->stack) {   // x[:, -L:] of the embedded input
       for (int k = tid; k < L * D; k += 256) {
         const int t = k / D, c = k - t * D;
-        X[t * ldD + c] = E0[(L0 - L + t) * ldD + c];
+        lsm[X + t * ldD + c] = lsm[E0 + (L0 - L + t) * ldD + c];
       }
       __syncthreads();
+      LWF_ST(3)
     }
     for (int l = 0; l < p->nl[i]; ++l) {
       const FEnc* ly = &p->enc[i][l];
-      fgemm(blob, pw, ly->qkv, X, ldD, 0, 0, L, T, ldT, nullptr, 0, false);
+      fgemm<0>(blob, pw, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
       __syncthreads();
+      LWF_ST(0)
       {
         const int call = ly->call;
         const int u = call >= 0 ? p->call_u[call] : L;
@@ -325,34 +377,43 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
               u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
       }
       __syncthreads();
-      fgemm(blob, pw, ly->o, CTX, ldH, 0, 0, L, X, ldD, nullptr, 0, true);   // x + attention (encoder.py:44-49)
+      LWF_ST(1)
+      fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
       __syncthreads();
+      LWF_ST(0)
       fln(X, ldD, L, D, blob + ly->g1, blob + ly->b1, X, ldD);
       __syncthreads();
-      fgemm(blob, pw, ly->f1, X, ldD, 0, 0, L, T, ldF, nullptr, p->act, false);
+      LWF_ST(2)
+      fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
       __syncthreads();
-      fgemm(blob, pw, ly->f2, T, ldF, 0, 0, L, X, ldD, nullptr, 0, true);
+      LWF_ST(0)
+      fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
       __syncthreads();
+      LWF_ST(0)
       fln(X, ldD, L, D, blob + ly->g2, blob + ly->b2, X, ldD);
       __syncthreads();
+      LWF_ST(2)
       if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
-        fgemm(blob, pw, ly->cv, X, ldD, 1, D, L, T, ldF, nullptr, 3, false);
+        fgemm<1>(blob, pw, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
         __syncthreads();
+        LWF_ST(0)
         const int Lo = ly->Lo;
         for (int k = tid; k < Lo * D; k += 256) {
           const int t = k / D, c = k - t * D;
-          float v = T[(2 * t) * ldF + c];
-          if (2 * t + 1 < L) v = fmaxf(v, T[(2 * t + 1) * ldF + c]);
-          if (2 * t - 1 >= 0) v = fmaxf(v, T[(2 * t - 1) * ldF + c]);
-          X[t * ldD + c] = v;
+          float v = lsm[T + (2 * t) * ldF + c];
+          if (2 * t + 1 < L) v = fmaxf(v, lsm[T + (2 * t + 1) * ldF + c]);
+          if (2 * t - 1 >= 0) v = fmaxf(v, lsm[T + (2 * t - 1) * ldF + c]);
+          lsm[X + t * ldD + c] = v;
         }
         __syncthreads();
+        LWF_ST(3)
         L = Lo;
       }
     }
     // Encoder.norm → rows [eoff, eoff + L) of the concatenated stack output
     fln(X, ldD, L, D, blob + p->ng[i], blob + p->nb[i], ENC + p->eoff[i] * ldD, ldD);
     __syncthreads();
+    LWF_ST(2)
   }
   // ---- decoder
   {
@@ -360,19 +421,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     const float* xd = x_dec + (size_t)b * Ld * Cd;
     for (int i = tid; i < Ld * Cd; i += 256) {
       const int t = i / Cd;
-      T[t * ldIN + (i - t * Cd)] = xd[i];
+      lsm[T + t * ldIN + (i - t * Cd)] = xd[i];
     }
   }
   __syncthreads();
-  fgemm(blob, pw, p->emb_d, T, p->ldINd, 1, p->Cd, Ld, XD, ldD, blob + p->pe_d, 0, false);
+  LWF_ST(3)
+  fgemm<1>(blob, pw, p->emb_d, T, p->ldINd, p->Cd, Ld, XD, ldD, blob + p->pe_d, 0, 0);
   __syncthreads();
+  LWF_ST(0)
   const int S = p->S;
-  float* QC = T;
-  float* KV = T + ((Ld + 15) & ~15) * ldH;
+  const int QC = T, KV = T + ((Ld + 15) & ~15) * ldH;
   for (int l = 0; l < p->ndec; ++l) {
     const FDec* ly = &p->dec[l];
-    fgemm(blob, pw, ly->qkv, XD, ldD, 0, 0, Ld, T, ldT, nullptr, 0, false);
+    fgemm<0>(blob, pw, ly->qkv, XD, ldD, 0, Ld, T, ldT, nullptr, 0, 0);
     __syncthreads();
+    LWF_ST(0)
     {
       const int call = ly->call;
       const int u = call >= 0 ? p->call_u[call] : Ld;
@@ -381,31 +444,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
             call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
     }
     __syncthreads();
-    fgemm(blob, pw, ly->o, CTX, ldH, 0, 0, Ld, XD, ldD, nullptr, 0, true);   // norm1(x + self-attention)
+    LWF_ST(1)
+    fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
     __syncthreads();
+    LWF_ST(0)
     fln(XD, ldD, Ld, D, blob + ly->g1, blob + ly->b1, XD, ldD);
     __syncthreads();
-    fgemm(blob, pw, ly->cq, XD, ldD, 0, 0, Ld, QC, ldH, nullptr, 0, false);
-    fgemm(blob, pw, ly->ckv, ENC, ldD, 0, 0, S, KV, ldKV, nullptr, 0, false);
+    LWF_ST(2)
+    fgemm<0>(blob, pw, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
+    fgemm<0>(blob, pw, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
     __syncthreads();
+    LWF_ST(0)
     fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr);
     __syncthreads();
-    fgemm(blob, pw, ly->co, CTX, ldH, 0, 0, Ld, XD, ldD, nullptr, 0, true);   // norm2(x + cross-attention)
+    LWF_ST(1)
+    fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
     __syncthreads();
+    LWF_ST(0)
     fln(XD, ldD, Ld, D, blob + ly->g2, blob + ly->b2, XD, ldD);
     __syncthreads();
-    fgemm(blob, pw, ly->f1, XD, ldD, 0, 0, Ld, T, ldF, nullptr, p->act, false);
+    LWF_ST(2)
+    fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
     __syncthreads();
-    fgemm(blob, pw, ly->f2, T, ldF, 0, 0, Ld, XD, ldD, nullptr, 0, true);   // norm3(x + y)
+    LWF_ST(0)
+    fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
     __syncthreads();
+    LWF_ST(0)
     fln(XD, ldD, Ld, D, blob + ly->g3, blob + ly->b3, XD, ldD);
     __syncthreads();
+    LWF_ST(2)
   }
   fln(XD, ldD, Ld, D, blob + p->dng, blob + p->dnb, XD, ldD);
   __syncthreads();
+  LWF_ST(2)
   // projection of the last pred_len rows → out[b][pred][c_out]
-  fgemm(blob, pw, p->proj, XD, ldD, 0, 0, Ld, nullptr, 0, nullptr, 0, false,
-        out + (size_t)b * p->pred * p->c_out, Ld - p->pred, p->c_out);
+  fgemm<0>(blob, pw, p->proj, XD, ldD, 0, Ld, 0, 0, nullptr, 0, 0, out + (size_t)b * p->pred * p->c_out, Ld - p->pred,
+           p->c_out);
+  LWF_ST(0)
+  LWF_ST_END
 }
 
 int prepare_fused() {

@@ -221,13 +221,13 @@ def test_fused_layerwise_equals_operator_launches():
     m = model_for(case)
     fused, _, _ = run_engine(m, xe, xd, case.idx)
     assert m.engine(torch.device("cuda:0")).last_path() == "layerwise-fused"
-    os.environ["CET_LW_FUSED"] = "0"
+    os.environ["CET_LW_FUSED"] = "0"   # read when the engine uploads its weights (first forward)
     try:
         m2 = model_for(case)
         eng2 = m2.engine(torch.device("cuda:0"))
+        ops, _, _ = run_engine(m2, xe, xd, case.idx)
     finally:
         del os.environ["CET_LW_FUSED"]
-    ops, _, _ = run_engine(m2, xe, xd, case.idx)
     assert eng2.last_path() == "layerwise"
     assert rel_nmse(fused, ops) < 1e-11, rel_nmse(fused, ops)
     run_engine(m, case.z["x_enc"], case.z["x_dec"], case.idx, attns=True)
