@@ -32,7 +32,6 @@ namespace lw {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int FMT = F_LMAX / 16;   // m-tiles per sequence
 constexpr int KW = 4;              // k-quads (16 k each) of weights per register window
 
 __device__ __forceinline__ float fgelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
@@ -56,6 +55,12 @@ __device__ __forceinline__ float dpp_f(float v, int ctrl) {
     default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
   }
 }
+__device__ __forceinline__ float row16_sum(float v) {   // over the 16 lanes of each DPP row
+  v += dpp_f(v, 0xB1);
+  v += dpp_f(v, 0x4E);
+  v += dpp_f(v, 0x141);
+  return v + dpp_f(v, 0x140);
+}
 __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f(v, 0xB1);    // quad_perm [1,0,3,2]
   v += dpp_f(v, 0x4E);    // quad_perm [2,3,0,1]
@@ -71,84 +76,113 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // Y[t][n] = act(Σ_k A(t, k)·W[n][k] · scale[n] + bias[n] + pe[t][n]) (+ Y[t][n] if res), t < L, n < N.
 // A and Y are LDS float offsets.  AMODE 0: A(t, k) = A[t·lda + k]; AMODE 1: circular k=3 conv,
 // A(t, tap·Cin + c) = A[((t − 1 + tap) mod L)·lda + c].  gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in
-// HBM instead of Y.
-template <int AMODE>
-__device__ __noinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
-                                   int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
-                                   int act, int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
+// HBM instead of Y.  MT = ceil(L / 16) m-tiles, a compile-time count: the K loop is straight-line code
+// (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A reads of k ≥ K land
+// in the padded, finite part of the LDS image and meet zero weights.
+template <int AMODE, int MT>
+__device__ __noinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
+                                     int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
+                                     int act, int res, float* __restrict__ gout, int t0, int ldo) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   const int r16 = lane & 15, q4 = lane >> 4;
   const int N = uni(g.N), K = uni(g.K);
   A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
-  const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4, MT = (L + 15) >> 4;
+  const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4;
   const bool has_b = uni(g.b) != (int)FNONE, has_s = uni(g.s) != (int)FNONE;
+  // the lane's A rows (AMODE 0) / its three circular source rows per m-tile (AMODE 1)
+  int rowoff[MT][3];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    int t = 16 * m + r16;
+    if (AMODE) {
+      t = t < L ? t : L - 1;
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {
+        int r = t - 1 + tap;
+        r = r < 0 ? r + L : (r >= L ? r - L : r);
+        rowoff[m][tap] = A + r * lda;
+      }
+    } else {
+      rowoff[m][0] = rowoff[m][1] = rowoff[m][2] = A + t * lda;
+    }
+  }
   for (int nt = w; nt < NT; nt += 4) {
     const int n = 16 * nt + r16;
     // epilogue vectors requested before the K loop (their latency hides under the MFMAs)
     const float sc = has_s && n < N ? blob[g.s + n] : 1.f;
     const float bi = has_b && n < N ? blob[g.b + n] : 0.f;
-    f32x4 acc[FMT];
+    f32x4 acc[MT];
 #pragma unroll
-    for (int m = 0; m < FMT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
     const f32x4* wp = reinterpret_cast<const f32x4*>(pw + g.w) + (size_t)nt * KQ * 64 + lane;
     // weights of KW k-quads in registers, the next window's loads in flight during this window's MFMAs
     f32x4 wa[KW], wb[KW];
 #pragma unroll
-    for (int i = 0; i < KW; ++i) wa[i] = i < KQ ? wp[(size_t)i * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < KW; ++i) wa[i] = wp[(size_t)(i < KQ ? i : 0) * 64];
     for (int kc = 0; kc < KQ; kc += KW) {
 #pragma unroll
-      for (int i = 0; i < KW; ++i) wb[i] = kc + KW + i < KQ ? wp[(size_t)(kc + KW + i) * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < KW; ++i) {
+        const int kq = kc + KW + i;
+        wb[i] = wp[(size_t)(kq < KQ ? kq : 0) * 64];
+      }
 #pragma unroll
       for (int i = 0; i < KW; ++i) {
+        if (kc + i < KQ) {
+          float av[4][MT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = 16 * (kc + i) + 4 * j + q4;
-          const bool kv = k < K;
-          int tap = 0, c = k;
-          if (AMODE) {
-            tap = (k >= Cin) + (k >= 2 * Cin);
-            c = k - tap * Cin;
-          }
-#pragma unroll
-          for (int m = 0; m < FMT; ++m) {
-            if (m < MT) {
-              int t = 16 * m + r16;
-              if (AMODE) {
-                t = t < L ? t : L - 1;
-                int r = t - 1 + tap;
-                r = r < 0 ? r + L : (r >= L ? r - L : r);
-                t = r;
-              }
-              const float a = kv ? lsm[A + t * lda + c] : 0.f;
-              acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wa[i][j], acc[m], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) {
+            const int k = 16 * (kc + i) + 4 * j + q4;
+            int tap = 0, c = k;
+            if (AMODE) {
+              tap = (k >= Cin) + (k >= 2 * Cin);
+              c = k - tap * Cin;
             }
+#pragma unroll
+            for (int m = 0; m < MT; ++m) av[j][m] = lsm[(AMODE ? (tap == 0 ? rowoff[m][0] : tap == 1 ? rowoff[m][1] : rowoff[m][2]) : rowoff[m][0]) + c];
           }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][m], wa[i][j], acc[m], 0, 0, 0);
         }
       }
 #pragma unroll
       for (int i = 0; i < KW; ++i) wa[i] = wb[i];
     }
-    // epilogue: lane holds rows 16m + 4·q4 + r, column n
     if (n >= N) continue;
 #pragma unroll
-    for (int m = 0; m < FMT; ++m) {
-      if (m < MT) {
+    for (int m = 0; m < MT; ++m) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int t = 16 * m + 4 * q4 + r;
-          if (t >= L) continue;
-          float y = acc[m][r] * sc + bi;
-          if (pe) y += pe[t * N + n];
-          y = act_of(y, act);
-          if (res) y += lsm[Y + t * ldy + n];
-          if (gout) {
-            if (t >= t0) gout[(t - t0) * ldo + n] = y;
-          } else {
-            lsm[Y + t * ldy + n] = y;
-          }
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * m + 4 * q4 + r;
+        if (t >= L) continue;
+        float y = acc[m][r] * sc + bi;
+        if (pe) y += pe[t * N + n];
+        y = act_of(y, act);
+        if (res) y += lsm[Y + t * ldy + n];
+        if (gout) {
+          if (t >= t0) gout[(t - t0) * ldo + n] = y;
+        } else {
+          lsm[Y + t * ldy + n] = y;
         }
       }
     }
+  }
+}
+
+template <int AMODE>
+__device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g, int A,
+                                      int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe, int act,
+                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
+  switch ((L + 15) >> 4) {
+    case 1: fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 2: fgemm_t<AMODE, 2>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 3: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 4: fgemm_t<AMODE, 4>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 5: fgemm_t<AMODE, 5>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 6: fgemm_t<AMODE, 6>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 7: fgemm_t<AMODE, 7>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    default: fgemm_t<AMODE, 8>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
   }
 }
 
@@ -158,7 +192,47 @@ __device__ __noinline__ void fln(int X, int ldx, int L, int D, const float* __re
                                  const float* __restrict__ bb, int Y, int ldy) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   X = uni(X); ldx = uni(ldx); L = uni(L); D = uni(D); Y = uni(Y); ldy = uni(ldy);
-  for (int t = w; t < L; t += 4) {
+  if (D <= 256) {   // four rows per wave at a time, 16 lanes per row
+    const int r16 = lane & 15, sub = lane >> 4;
+    float gv[16], bv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = r16 + 16 * i;
+      gv[i] = c < D ? g[c] : 0.f;
+      bv[i] = c < D ? bb[c] : 0.f;
+    }
+    for (int t0 = 4 * w; t0 < L; t0 += 16) {
+      const int t = t0 + sub;
+      const bool on = t < L;
+      const int x = X + (on ? t : t0) * ldx;
+      float v[16];
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = r16 + 16 * i;
+        v[i] = c < D ? lsm[x + c] : 0.f;
+        s += v[i];
+      }
+      const float mean = row16_sum(s) / (float)D;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float d = r16 + 16 * i < D ? v[i] - mean : 0.f;
+        q = fmaf(d, d, q);
+      }
+      const float inv = 1.0f / sqrtf(row16_sum(q) / (float)D + 1e-5f);
+      if (on) {
+        const int y = Y + t * ldy;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int c = r16 + 16 * i;
+          if (c < D) lsm[y + c] = (v[i] - mean) * inv * gv[i] + bv[i];
+        }
+      }
+    }
+    return;
+  }
+  for (int t = w; t < L; t += 4) {   // one row per wave
     const int x = X + t * ldx;
     float s = 0.f;
     for (int c = lane; c < D; c += 64) s += lsm[x + c];
@@ -249,24 +323,50 @@ __device__ __noinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int
       wave_lds_sync();
     }
     const int nsel = sparse ? u : LQ;
-    // ---- softmax(scale · S) of the selected rows, P over S (zero beyond the row's last key)
-    for (int r = lane; r < nsel; r += 64) {
-      const int q = sparse ? sel[r] : r;
+    // ---- softmax(scale · S) of the selected rows, P over S (zero beyond the row's last key).  Up to 32
+    //      rows: lanes l and l + 32 share row l & 31, each taking every other key, combined by the
+    //      32-lane swap; more rows: one lane per row.
+    if (nsel <= 32) {
+      const int r = lane & 31, half = lane >> 5;
+      const bool act = r < nsel;
+      const int q = act ? (sparse ? sel[r] : r) : 0;
       float* row = S + q * SS;
-      const int kmax = causal ? q + 1 : LK;
+      const int kmax = !act ? 0 : (causal ? q + 1 : LK);
       float mx = -INFINITY;
-#pragma unroll 8
-      for (int j = 0; j < kmax; ++j) mx = fmaxf(mx, row[j] * scale);
+#pragma unroll 4
+      for (int j = half; j < kmax; j += 2) mx = fmaxf(mx, row[j] * scale);
+      mx = swap_pair_max32(mx);
       float sum = 0.f;
-#pragma unroll 8
-      for (int j = 0; j < LKp; ++j) {
+      const int kend = act ? LKp : 0;
+#pragma unroll 4
+      for (int j = half; j < kend; j += 2) {
         const float p = j < kmax ? expf(row[j] * scale - mx) : 0.f;
         row[j] = p;
         sum += p;
       }
+      sum = swap_pair_sum32(sum);
       const float inv = 1.0f / sum;
+#pragma unroll 4
+      for (int j = half; j < kmax; j += 2) row[j] *= inv;
+    } else {
+      for (int r = lane; r < nsel; r += 64) {
+        const int q = sparse ? sel[r] : r;
+        float* row = S + q * SS;
+        const int kmax = causal ? q + 1 : LK;
+        float mx = -INFINITY;
 #pragma unroll 8
-      for (int j = 0; j < kmax; ++j) row[j] *= inv;
+        for (int j = 0; j < kmax; ++j) mx = fmaxf(mx, row[j] * scale);
+        float sum = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < LKp; ++j) {
+          const float p = j < kmax ? expf(row[j] * scale - mx) : 0.f;
+          row[j] = p;
+          sum += p;
+        }
+        const float inv = 1.0f / sum;
+#pragma unroll 8
+        for (int j = 0; j < kmax; ++j) row[j] *= inv;
+      }
     }
     wave_lds_sync();
     // ---- the initial context of the unselected rows: mean(V) (attn.py:116-119) or cumsum(V) (:120-125)
