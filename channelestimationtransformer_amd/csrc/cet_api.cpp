@@ -135,10 +135,8 @@ struct cet_engine {
   bool dirty = true;
   bool uploaded = false;
   int last_path = 0; // the fused kernel the last forward launched (CET_PATH_*), 0: none yet
-  int v5_min_b = 1;  // smallest batch v5 runs (CET_V5_MIN_B); smaller ones go to v4
   bool enc_split_ok = true;   // v4 encoder split allowed (CET_NO_ENC_SPLIT at creation turns it off)
-  int variant = 4;   // fused-kernel generation: 4 (one sequence per workgroup, default) or 5 (two per
-                     // workgroup where the plan allows; CET_KERNEL=v5)
+  int variant = 4;   // fused-kernel generation: 4 (one sequence per workgroup), the only one kept
   // shapes outside the fused kernels (d_model != 128, n_heads != 8, d_ff > 128, ...): the layer-wise
   // engine (cet_lw.hip), fp32 on the f32 MFMA, one launch per operator
   bool generic = false;
@@ -812,25 +810,6 @@ int build_informer(cet_engine* e) {
     if (LMAX * p.in_stride * 4 > v4_ctx_bytes(P) || Ld > 48 || p.lds4_bytes_replay > 160 * 1024)
       return fail(CET_E_INVALID, "v4 LDS layout: staged input, decoder length or LDS size out of range");
   }
-  // v5 (two sequences per workgroup, bf16 policy): the fixed per-sequence regions and the shared table
-  // (cet_plan.hpp v5_fixed), then per sequence the stack output, the staged x_dec and the labels, then
-  // the sampler state; v5_ok = 0 routes the plan to v4
-  {
-    const int RS = v4_rs(0);
-    p.lds5_enc = v5_fixed(0, V5_NS);
-    p.lds5_enc_stride = al(SP * RS);
-    p.lds5_zero = p.lds5_enc + V5_NS * p.lds5_enc_stride;
-    p.lds5_xdec = p.lds5_zero;
-    p.lds5_xdec_stride = al(Ld * p.in_stride * 4);
-    p.lds5_lab = p.lds5_xdec + V5_NS * p.lds5_xdec_stride;
-    p.lds5_lab_stride = al(c.out_len * c.c_out * 4);
-    p.lds5_bytes = p.lds5_lab + V5_NS * p.lds5_lab_stride;
-    p.lds5_mt = p.lds5_bytes;
-    p.lds5_bytes_replay = al(p.lds5_mt + MT_WORDS_HOST * 4);
-    // one f32x4 of x_enc / x_dec / labels per thread at kernel entry (512 threads)
-    p.v5_ok = P == 0 && p.lds5_bytes_replay <= 160 * 1024 && c.seq_len * c.enc_in <= 4 * 512 &&
-              Ld * c.dec_in <= 4 * 512 && c.out_len * c.c_out <= 4 * 512 && c.c_out <= 16;
-  }
   p.stack = c.stack;
   return CET_OK;
 }
@@ -1295,9 +1274,6 @@ int cet_create_informer(const cet_informer_config* cfg, cet_engine** out) {
   e->kind = 0;
   e->icfg = *cfg;
   e->generic = !fused_supported(*cfg) || std::getenv("CET_LAYERWISE") != nullptr;
-  if (const char* v = std::getenv("CET_KERNEL"))
-    e->variant = std::strcmp(v, "v5") == 0 ? 5 : 4;
-  if (const char* v = std::getenv("CET_V5_MIN_B")) e->v5_min_b = std::max(1, std::atoi(v));
   e->enc_split_ok = std::getenv("CET_NO_ENC_SPLIT") == nullptr;
   schema_informer(e.get());
   // shapes of the ProbSparse draws are known before weights arrive
@@ -1476,18 +1452,12 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   b.enc_xchg = nullptr;
   b.enc_count = nullptr;
   const bool diag = a.attns || a.dbg || a.stamps;
-  const bool v4_only = a.attns != nullptr;   // attention maps: the v4 DIAG instance
   const bool replay = a.mt_in && !a.cnt;
   // encoder split (v4): the encoders of a stack are independent until the decoder, so at small batches
   // each runs on its own workgroup (bf16 policy, no ProbSparse draws, production outputs only, the
   // whole grid resident at two workgroups per CU)
   const bool split = e->enc_split_ok && e->prec == 0 && p.n_enc > 1 && p.n_calls == 0 && !diag &&
                      (int64_t)a.B * p.n_enc <= 512;
-  // v5: two sequences per workgroup (bf16 policy, production outputs, the plan fits its LDS layout)
-  if (e->variant == 5 && p.v5_ok && e->prec == 0 && !v4_only && !split && a.B >= e->v5_min_b) {
-    e->last_path = CET_PATH_V5;
-    return cet_launch_informer_v5(&b, e->prec, e->icfg.d_ff, replay ? p.lds5_bytes_replay : p.lds5_bytes, st);
-  }
   if (split) {
     const size_t words = (size_t)a.B * p.S * (v4_rs(0) / 8);
     if (words > e->enc_xchg_n) {
@@ -1781,9 +1751,8 @@ int cet_set_sampler(cet_engine* e, int on_host) {
 
 int cet_set_variant(cet_engine* e, int variant) {
   if (!e) return fail(CET_E_INVALID, "null engine");
-  if (variant != 4 && variant != 5)
-    return fail(CET_E_INVALID, "variant must be 4 (one sequence per workgroup) or 5 (two); 1-3 are retired");
-  if (e->kind != 0 && variant != 4) return fail(CET_E_INVALID, "the Transformer engine has variant 4 only");
+  if (variant != 4)
+    return fail(CET_E_INVALID, "variant must be 4 (one sequence per workgroup); 1-3 and 5 are retired");
   e->variant = variant;
   return CET_OK;
 }

@@ -1,6 +1,6 @@
 // Device-side building blocks of the fused channel-predictor kernels (gfx950 / CDNA4).
 //
-// Conventions shared by the fused kernels (cet_v4.hpp / cet_v5.hpp):
+// Conventions shared by the fused kernels (cet_v4.hpp, cet_transformer4.hip):
 //  * Dense layers are computed TRANSPOSED: Yᵀ[n][m] = W[n][k] · Xᵀ[k][m] on
 //    v_mfma_f32_16x16x32_bf16.  W (the A operand) is pre-packed on the host in
 //    fragment order [n_tile][k_step][lane][8] so one wave loads a 16×32 weight
@@ -67,8 +67,10 @@ __device__ __forceinline__ bf16x4 cvt4(const f32x4& v) {
 // XOR-butterfly reductions across the lane axis.  The 16- and 32-lane exchanges use gfx950's
 // v_permlane16_swap / v_permlane32_swap (one VALU op, no LDS); with both operands = v the two
 // results are v and its partner, in some order per lane, so their sum/max is the butterfly.
-// Caution (cet_v5.hpp bp_sum): the compiler does not keep these swaps out of EXEC-narrowed code; the
-// v4 kernels' outputs are checked bit for bit against the ds_bpermute form (v5) in the GPU tests.
+// Caution: a butterfly is only right when every lane takes part, and the compiler once sank such swaps
+// into EXEC-narrowed code (the retired two-sequence kernel, profiles/r03/bisect_*.txt).  Every call sits
+// at full EXEC in the source; tools/exec_scan.py checks the built code objects for a swap reached under
+// a narrowed EXEC (tests/test_isa_guard.py, CPU suite).
 __device__ __forceinline__ float swap_pair_sum16(float v) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);

@@ -62,7 +62,16 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   float* LAB = reinterpret_cast<float*>(lds + PL.lds4_lab);
   const int nlab = PL.pred_len * PL.c_out;
   f32x4 lb4 = {0.f, 0.f, 0.f, 0.f};
-  if (a.label && t4 < nlab) lb4 = *reinterpret_cast<const f32x4*>(a.label + (size_t)b * nlab + t4);
+  if (a.label && t4 < nlab) {
+    // nlab need not be a multiple of 4 (c_out ≤ 16 is any width): element loads, never past the batch
+    const float* lp = a.label + (size_t)b * nlab + t4;
+    if ((nlab & 3) == 0) {
+      lb4 = *reinterpret_cast<const f32x4*>(lp);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lb4[j] = t4 + j < nlab ? lp[j] : 0.f;
+    }
+  }
   // zero the activation images: rows past L are read (never used) by MFMAs
   for (int i = threadIdx.x; i < PL.lds4_zero / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -87,7 +87,6 @@ bool ensure_lds_attr(const void* kern);
 extern "C" int cet_launch_sampler_prep(const cet::InformerPlan* plan, const uint32_t* mt_in, uint32_t* mt_out,
                                        uint8_t* tab_out, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_informer_v4(const cet::InformerArgs* a, int prec, int dff, int lds_bytes, hipStream_t stream);
-extern "C" int cet_launch_informer_v5(const cet::InformerArgs* a, int prec, int dff, int lds_bytes, hipStream_t stream);
 extern "C" int cet_launch_prepare_batch(const void* args, hipStream_t stream);
 extern "C" int cet_launch_synth(const void* args, hipStream_t stream);
 extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff, int lds_bytes, hipStream_t stream);

@@ -61,6 +61,9 @@ int Model::build_fused() {
   if (why) fprintf(stderr, "lw fused: nenc %d ndec %d calls %zu Lm %d S %d\n", nenc, ndec, call_u.size(), Lm, S);
   if (nenc < 1 || nenc > F_MAX_ENC || ndec > F_MAX_DEC || (int)call_u.size() > F_MAX_CALLS) return 0;
   if (Lm > F_LMAX || S > F_LMAX || S < 1) return 0;
+  // the validated range (tests/test_gpu_layerwise.py: up to 48 rows = 3 m-tiles, d_model ≤ 256 for the
+  // 16-lane LayerNorm rows); wider shapes keep the operator launches
+  if (Lm > 48 || D > 256) return 0;
   for (const auto& e : enc)
     if ((int)e.size() > F_MAX_EL) return 0;
   auto r16 = [](int x) { return (x + 15) & ~15; };

@@ -335,7 +335,8 @@ __device__ __noinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int
       float mx = -INFINITY;
 #pragma unroll 4
       for (int j = half; j < kmax; j += 2) mx = fmaxf(mx, row[j] * scale);
-      mx = swap_pair_max32(mx);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));   // ds_bpermute: the scan (tools/exec_scan.py) cannot follow
+                                                 // this function's spilled EXEC masks to clear a swap here
       float sum = 0.f;
       const int kend = act ? LKp : 0;
 #pragma unroll 4
@@ -344,7 +345,7 @@ __device__ __noinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int
         row[j] = p;
         sum += p;
       }
-      sum = swap_pair_sum32(sum);
+      sum += __shfl_xor(sum, 32, 64);
       const float inv = 1.0f / sum;
 #pragma unroll 4
       for (int j = half; j < kmax; j += 2) row[j] *= inv;

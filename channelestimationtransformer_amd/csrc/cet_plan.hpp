@@ -91,11 +91,6 @@ struct InformerPlan {
   int lds4_enc, lds4_enc_lo, lds4_cnt, lds4_mt, lds4_zero, lds4_bytes, lds4_bytes_replay;
   int lds4_xdec;            // x_dec staged at kernel entry (byte offset), or -1: staged before the decoder
   int lds4_lab;             // labels of the fused NMSE (pred_len × c_out fp32), staged at kernel entry
-  // v5 layout (cet_v5.hpp L5: NS sequences per workgroup): after the fixed per-sequence regions and
-  // the shared multiplicity table, per sequence the stack output, the staged x_dec and the labels, then
-  // the sampler state (in-kernel replay only); v5_ok = 0 when the plan does not fit (v4 runs it)
-  int lds5_enc, lds5_enc_stride, lds5_xdec, lds5_xdec_stride, lds5_lab, lds5_lab_stride;
-  int lds5_zero, lds5_mt, lds5_bytes, lds5_bytes_replay, v5_ok;
   int prec;                 // v4 operand precision of the dense layers (v4::P_BF16 / P_X3 / P_FP8)
   int stack;
   int in_stride;            // floats per staged input row
@@ -130,12 +125,6 @@ constexpr int v4_enc(int P) { return v4_cnt(P) + LMAX * 96; }               // s
 static_assert(LMAX * LN3_STRIDE * 4 + LMAX * 8 <= 8 * V2_SCR_FLOATS * 4,
               "LN partials and row statistics fit the scratch they alias");
 static_assert(v4_ctx(0) % 16 == 0 && v4_scr(0) % 16 == 0 && v4_enc(1) % 16 == 0 && v4_enc(2) % 16 == 0, "16-B");
-
-// v5 layout (cet_v5.hpp L5): per sequence image | context | attention scratch, NS times; then the
-// multiplicity table shared by the sequences; then the plan-sized regions (InformerPlan::lds5_*).
-constexpr int V5_NS = 2;   // sequences per workgroup
-constexpr int v5_seq(int P) { return v4_img(P) + v4_ctx_bytes(P) + 8 * V2_SCR_FLOATS * 4; }
-constexpr int v5_fixed(int P, int ns) { return ns * v5_seq(P) + LMAX * 96; }
 
 // LDS bytes of the three-pass sampler replay (cet_sampler.hpp replay_all_fast): the padded
 // mt19937 state | the forward's tempered words | every call's multiplicity table.

@@ -148,6 +148,12 @@ class Engine:
         for t in (x_enc, x_dec, out):
             if t.dtype != torch.float32 or not t.is_contiguous():
                 raise ValueError("x_enc, x_dec and out must be contiguous float32")
+        if int(x_dec.shape[0]) != B or int(out.shape[0]) != B:
+            raise ValueError("x_enc, x_dec and out must have the same batch size")
+        dev = x_enc.device
+        for t in (x_dec, out, label, nmse_sums):
+            if t.device != dev or not t.is_cuda:
+                raise ValueError(f"every tensor must be on the engine's device {dev}")
         if stream is None:
             stream = _stream_ptr(x_enc.device)
         f, h = lib.cet_forward_nmse, self._h
@@ -155,6 +161,8 @@ class Engine:
                [ctypes.c_void_p(t.data_ptr()) for t in (out, label)] + [None]
         s0, stride, n = nmse_sums.data_ptr(), 2 * T * 8, int(nmse_sums.shape[0])
         st = ctypes.c_void_p(stream)
+        # the step keeps the engine and every bound tensor alive: the launch writes through raw pointers
+        keep = (self, x_enc, x_dec, out, label, nmse_sums)
 
         def step(k: int) -> None:
             if not 0 <= k < n:
@@ -163,6 +171,7 @@ class Engine:
             if rc < 0:
                 check(rc, "cet_forward_nmse")
 
+        step.keepalive = keep
         return step
 
     def attns_floats(self) -> int:
@@ -184,15 +193,14 @@ class Engine:
         check(lib.cet_set_sampler(self._h, int(bool(on_host))), "cet_set_sampler")
 
     def set_variant(self, variant: int) -> None:
-        """Fused-kernel generation: 4 (default: one sequence per workgroup; every precision policy and the
-        diagnostic outputs) or 5 (two sequences per workgroup where the plan allows, bit-for-bit v4's
-        outputs)."""
+        """Fused-kernel generation: 4, the only one kept (one sequence per workgroup; every precision policy
+        and the diagnostic outputs); 1-3 and 5 are retired (CET_E_INVALID)."""
         check(lib.cet_set_variant(self._h, int(variant)), "cet_set_variant")
 
-    PATHS = {0: None, 3: "layerwise", 4: "v4", 5: "v5", 31: "layerwise-fused", 41: "v4-split"}
+    PATHS = {0: None, 3: "layerwise", 4: "v4", 31: "layerwise-fused", 41: "v4-split"}
 
     def last_path(self):
-        """The kernel path the last Informer forward took: "v5", "v4", "v4-split", "layerwise" (operator
+        """The kernel path the last Informer forward took: "v4", "v4-split", "layerwise" (operator
         launches), "layerwise-fused" (the layer-wise forward in one launch) or None."""
         return self.PATHS[check(lib.cet_last_path(self._h), "cet_last_path")]
 

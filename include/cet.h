@@ -118,20 +118,16 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen);
 /* Diagnostics (DIAG kernel instance): per-phase s_memtime stamps into a device buffer of B·128 uint64. */
 int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev);
 
-/* Select the fused-kernel generation of an Informer engine: 4 (default: one sequence per 512-thread
+/* Select the fused-kernel generation of an Informer engine: 4, the only one (one sequence per 512-thread
  * workgroup, two workgroups per CU, every precision policy, the attention maps and the small-batch
- * encoder split) or 5 (TWO sequences per workgroup, one workgroup per CU, 256 VGPRs, every weight
- * fragment shared by both sequences; bf16 policy, production outputs, activation dumps and phase
- * stamps — other cases run generation 4; the same arithmetic per sequence, outputs bit-for-bit equal to
- * generation 4's).  CET_KERNEL=v5 in the environment selects 5 at creation; CET_V5_MIN_B=n sends
- * batches below n to generation 4.  Transformer engines have generation 4 only.  Generations 1-3 are
- * retired: CET_E_INVALID. */
+ * encoder split).  Generations 1-3 and 5 (two sequences per workgroup: measured slower)
+ * are retired: CET_E_INVALID. */
 int cet_set_variant(cet_engine* e, int variant);
-/* The kernel path the engine's last Informer forward took: CET_PATH_V5, CET_PATH_V4,
+/* The kernel path the engine's last Informer forward took: CET_PATH_V4,
  * CET_PATH_V4_SPLIT (v4 with the stack's encoders on separate workgroups), CET_PATH_LW (layer-wise
  * operator launches), CET_PATH_LW_FUSED (the layer-wise forward fused into one launch, one workgroup
  * per sequence with its activations in LDS), 0 before any. */
-enum { CET_PATH_LW = 3, CET_PATH_V4 = 4, CET_PATH_V5 = 5, CET_PATH_LW_FUSED = 31, CET_PATH_V4_SPLIT = 41 };
+enum { CET_PATH_LW = 3, CET_PATH_V4 = 4, CET_PATH_LW_FUSED = 31, CET_PATH_V4_SPLIT = 41 };
 int cet_last_path(cet_engine* e);
 
 /* Operand precision of the v4 kernel's dense layers (Informer engines):

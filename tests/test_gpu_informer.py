@@ -36,12 +36,11 @@ def fixture_selection_mismatches(case, dbg):
     return n
 
 
-@pytest.mark.parametrize("instance", ["production", "production-v5", "diag", "diag-v5"])
+@pytest.mark.parametrize("instance", ["production", "diag"])
 @pytest.mark.parametrize("name", INFORMER_CASES)
 def test_informer_matches_reference_fixture(name, instance):
-    """Every reference fixture through every kernel instance: the production one (what bench.py and the
-    configs tool time: v4, one sequence per workgroup), the two-sequence v5 production instance, and the
-    diagnostic instances of both generations (activation dumps; every dumped stage is checked against
+    """Every reference fixture through both kernel instances: the production one (what bench.py and the
+    configs tool time) and the diagnostic one (activation dumps; every dumped stage is checked against
     the oracle), at the engine's automatic precision.  A genuinely sparse masked decoder
     (informer_prob_lab20: L=25, u=20, unselected rows take cumsum(V)) is output-discontinuous in the
     top-u selection, so the engine runs it in split bf16 (v4) and its selection must equal the
@@ -52,11 +51,8 @@ def test_informer_matches_reference_fixture(name, instance):
     case = load_case(name)
     m = model_for(case)
     eng = m.engine(torch.device("cuda:0"))
-    v5 = instance.endswith("-v5")
-    eng.set_variant(5 if v5 else 4)
-    diag = instance.startswith("diag")
+    diag = instance == "diag"
     out, dbg, _ = run_engine(m, case.z["x_enc"], case.z["x_dec"], case.idx, debug=diag)
-    eng.set_variant(4)
     rep, _, _ = stage_report(case, out, dbg)
     err = rel_nmse(out, case.z["out"])
     assert np.isfinite(out).all()
@@ -74,7 +70,7 @@ def test_informer_matches_reference_fixture(name, instance):
     elif split_ok:
         assert eng.last_path() == "v4-split"
     else:
-        assert eng.last_path() == ("v5" if v5 else "v4")
+        assert eng.last_path() == "v4"
     if diag:   # every dumped stage (embedding, each layer, conv, encoder norms, decoder layers) vs the oracle
         bad = {k: v for k, v in rep.items() if not k.startswith("M") and not v < 1e-3}
         assert not bad, bad
@@ -526,77 +522,6 @@ def test_nmse_split_kernel(shape):
     np.testing.assert_allclose(acc.cpu().numpy(), 3 * ref_split(p, y), rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [4, 5])
-def test_kernel_variants_agree_with_oracle(variant):
-    """Both fused-kernel generations (v4: one sequence per workgroup; v5: two) meet the bar."""
-    _gpu()
-    from channelestimationtransformer_amd.dataset import make_batch
-    from engine_util import model_for, run_engine
-    from golden_util import oracle_for
-
-    case = load_case("informer_prob_e43")
-    m = model_for(case)
-    eng = m.engine(torch.device("cuda:0"))
-    eng.set_variant(variant)
-    xe, xd, _ = make_batch(24, seed=41)
-    out, _, _ = run_engine(m, xe, xd, case.idx)
-    assert eng.last_path() == f"v{variant}"
-    ref, _ = oracle_for(case).forward(xe, xd, case.idx)
-    assert rel_nmse(out, ref) < TOL
-
-
-@pytest.mark.parametrize("name,B", [("informer_prob_b4", 512), ("informer_prob_b4", 37), ("informer_prob_e43", 64),
-                                    ("informer_single_e3", 33), ("informer_prob_seq48", 128), ("informer_lsq8", 96),
-                                    ("informer_full_e43", 600)])
-def test_v5_pairs_equal_v4_per_sequence(name, B):
-    """v5 carries two sequences per workgroup under shared weight fragments; each sequence's arithmetic
-    is v4's, so the outputs equal the one-sequence kernel's bit for bit (and meet the oracle).  Odd batches leave
-    the last workgroup's second slot a repeat whose outputs are dropped."""
-    _gpu()
-    from channelestimationtransformer_amd.dataset import make_batch
-    from engine_util import model_for, run_engine
-    from golden_util import oracle_for
-
-    case = load_case(name)
-    m = model_for(case)
-    cfg = case.cfg
-    eng = m.engine(torch.device("cuda:0"))
-    xe, xd, _ = make_batch(B, cfg["seq_len"], cfg["label_len"], cfg["pred_len"], seed=3000 + B)
-    eng.set_variant(5)
-    o5, _, _ = run_engine(m, xe, xd, case.idx)
-    assert eng.last_path() == "v5"
-    eng.set_variant(4)
-    o4, _, _ = run_engine(m, xe, xd, case.idx)
-    assert eng.last_path() == "v4"
-    assert np.isfinite(o5).all()
-    # each sequence goes through v4's arithmetic in the same order: bit-for-bit the same rows, in either
-    # slot of its workgroup (a first-slot deviation here once exposed a compiler reordering, cet_v5.hpp)
-    per = ((o5 - o4) ** 2).sum((1, 2)) / (o4 ** 2).sum((1, 2))
-    assert (per == 0).all(), (np.nonzero(per)[0][:8], float(per.max()))
-    rows = np.arange(B) if B <= 40 else np.r_[0:20, B - 20:B]
-    ref, _ = oracle_for(case).forward(xe[rows], xd[rows], case.idx)
-    assert rel_nmse(o5[rows], ref) < TOL
-
-
-def test_v5_slot_independence_is_bitwise():
-    """A sequence's result does not depend on its partner or on which slot of the workgroup it takes:
-    shards that shift the pairing (odd offsets) give bitwise-identical rows."""
-    _gpu()
-    from channelestimationtransformer_amd.dataset import make_batch
-    from engine_util import model_for, run_engine
-
-    case = load_case("informer_prob_b4")
-    m = model_for(case)
-    xe, xd, _ = make_batch(48, seed=8)
-    eng = m.engine(torch.device("cuda:0"))
-    eng.set_variant(5)
-    full, _, _ = run_engine(m, xe, xd, case.idx)
-    assert eng.last_path() == "v5"
-    parts = [run_engine(m, xe[a:b], xd[a:b], case.idx)[0] for a, b in ((0, 17), (17, 30), (30, 48))]
-    eng.set_variant(4)
-    np.testing.assert_array_equal(np.concatenate(parts), full)
-
-
 def test_weight_reload_keeps_the_stream():
     """A weight reload while prepared tables are pending (B >= 64 after a seed) must not skip a
     forward's draws: seed, forward, reload, forward — bitwise equal to explicit-index runs."""
@@ -753,26 +678,32 @@ def test_fused_nmse_matches_standalone(B, native):
     np.testing.assert_allclose(acc.cpu().numpy(), 3 * r, rtol=1e-5)
 
 
-@pytest.mark.parametrize("variant", [4, 5])
-def test_fused_nmse_both_generations(variant):
-    """The fused NMSE_Split epilogue and its last-workgroup reduction on both kernel generations (v5
-    counts workgroups of two sequences, an odd batch included)."""
+@pytest.mark.parametrize("c_out", [16, 3])
+def test_fused_nmse_odd_batch_and_label_width(c_out):
+    """The fused NMSE_Split epilogue and its last-workgroup reduction at an odd batch, and with a label row
+    (pred_len × c_out = 15 floats) that is not a whole number of 16-byte vectors: the labels are staged
+    with element loads, never past the batch's last row."""
     _gpu()
     from channelestimationtransformer_amd.dataset import make_batch
-    from engine_util import model_for
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.spec import informer_stack_spec
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
     from oracle.metrics_np import nmse_split as ref_split
 
-    case = load_case("informer_prob_b4")
-    m = model_for(case)
     dev = torch.device("cuda:0")
-    eng = m.engine(dev)
-    eng.set_variant(variant)
-    xe_np, xd_np, lab_np = make_batch(65, seed=3)
+    m = InformerStack(16, 16, c_out, 90, 10, 5, 5, 128, 8, [4], 3, 64, 0.05, "prob", "fixed", "gelu", False, True,
+                      dev)
+    state = synthetic_state_dict(informer_stack_spec(16, 16, c_out, 128, 8, [4], 3, 64, freq="gelu"), 3)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
+    eng = m.eval().engine(dev)
+    eng.seed(2)
+    B = 65
+    xe_np, xd_np, lab_np = make_batch(B, seed=3)
+    lab_np = np.ascontiguousarray(lab_np[..., :c_out])
     xe, xd, lab = (torch.from_numpy(a).to(dev) for a in (xe_np, xd_np, lab_np))
-    eng.set_indices(case.idx)
-    o = torch.empty(65, 5, 16, device=dev)
+    o = torch.empty(B, 5, c_out, device=dev)
     s = torch.zeros(2, 5, dtype=torch.float64, device=dev)
     eng.forward_nmse(xe, xd, o, lab, None, s)
     torch.cuda.synchronize()
-    assert eng.last_path() == f"v{variant}"
+    assert eng.last_path() == "v4"
     np.testing.assert_allclose((s[0] / s[1]).cpu().numpy(), ref_split(o.cpu().numpy(), lab_np), rtol=1e-5)

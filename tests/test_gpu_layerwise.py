@@ -260,3 +260,42 @@ def test_fused_layerwise_probsparse_vs_oracle(B):
     n = min(B, 64)
     ref, _ = orc.forward(xe[:n], xd[:n], idx)
     assert rel_nmse(out[:n], ref) < TOL, rel_nmse(out[:n], ref)
+
+
+@pytest.mark.parametrize("attn,seq_len,label_len,pred_len", [("full", 48, 10, 5), ("prob", 48, 25, 9)])
+def test_fused_layerwise_longer_shapes_vs_oracle(attn, seq_len, label_len, pred_len):
+    """The fused layer-wise form past the checkpoint's own shape, with the checkpoint's weights (they do
+    not depend on the lengths): seq_len 48 makes three m-tiles per GEMM; attn "full" gives 48 selected
+    rows (the one-lane-per-row softmax, nsel > 32); attn "prob" with label_len 25 + pred_len 9 gives a
+    genuinely sparse masked decoder (u = 5·ceil(ln 34) = 20 of 34 queries: unselected rows take cumsum(V),
+    with the mix re-view).  Explicit draws, fused form against the float64 oracle at fp32 level."""
+    _gpu()
+    import dataclasses
+
+    from engine_util import model_for, run_engine
+
+    from channelestimationtransformer_amd.rng import draw_indices
+    from oracle.informer_np import sample_shapes
+
+    base = load_case(CKPT)
+    meta = dict(base.meta)
+    meta["cfg"] = dict(base.cfg, attn=attn, seq_len=seq_len, label_len=label_len, pred_len=pred_len)
+    case = dataclasses.replace(base, meta=meta)
+    orc = oracle_for(case)
+    idx = draw_indices(sample_shapes(orc.cfg), seed=11)
+    m = model_for(case)
+    B = 37
+    xe, xd = _random_batch(case.cfg, B, 5)
+    out, _, _ = run_engine(m, xe, xd, idx)
+    assert m.engine(torch.device("cuda:0")).last_path() == "layerwise-fused"
+    ref, _ = orc.forward(xe, xd, idx)
+    assert rel_nmse(out, ref) < TOL, rel_nmse(out, ref)
+    # the same forward on the operator launches agrees with the fused form
+    os.environ["CET_LW_FUSED"] = "0"
+    try:
+        m2 = model_for(case)
+        out2, _, _ = run_engine(m2, xe, xd, idx)
+        assert m2.engine(torch.device("cuda:0")).last_path() == "layerwise"
+    finally:
+        del os.environ["CET_LW_FUSED"]
+    assert rel_nmse(out, out2) < 1e-10, rel_nmse(out, out2)

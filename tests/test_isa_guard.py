@@ -1,0 +1,65 @@
+"""Build guard (CPU): no cross-lane swap of the shipped gfx950 code runs under a narrowed EXEC.
+
+The v4 kernels and the fused layer-wise form reduce across lanes with v_permlane16_swap /
+v_permlane32_swap; a butterfly is only right when every lane takes part, and the compiler once sank
+such swaps into EXEC-narrowed code (v5's bisect, profiles/r03/bisect_*.txt).  tools/exec_scan.py runs a
+forward dataflow of the SI control-flow lowering's EXEC masks over every function of every code object
+in libcet.so and reports each swap reached inside an open divergent region.
+"""
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+LIB = os.path.join(ROOT, "channelestimationtransformer_amd", "libcet.so")
+
+pytestmark = pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"),
+                                reason="needs the ROCm llvm-objdump")
+
+
+def test_no_lane_swap_under_narrowed_exec_in_libcet():
+    import exec_scan
+
+    if not os.path.exists(LIB):
+        pytest.skip("libcet.so not built")
+    findings, counted = exec_scan.scan(LIB)
+    assert counted > 1000, f"only {counted} cross-lane swaps found: the scan did not see the v4 kernels"
+    assert not findings, "\n".join(" ".join(f) for f in findings[:20])
+
+
+def _fn(lines):
+    """A synthetic function body in llvm-objdump's format (4-byte instructions from 0x100)."""
+    out = ["0000000000000100 <f>:"]
+    for i, ins in enumerate(lines):
+        out.append(f"\t{ins:58s}// {0x100 + 4 * i:012X}: 00000000")
+    return "\n".join(out)
+
+
+@pytest.mark.parametrize("lines,flag", [
+    # a swap inside an if-region: flagged
+    (["v_cmp_gt_u32_e32 vcc, 16, v0", "s_and_saveexec_b64 s[4:5], vcc", "s_cbranch_execz 2",
+      "v_permlane16_swap_b32_e32 v1, v2", "s_or_b64 exec, exec, s[4:5]", "s_endpgm"], True),
+    # the same swap after the region is closed: clean
+    (["v_cmp_gt_u32_e32 vcc, 16, v0", "s_and_saveexec_b64 s[4:5], vcc", "s_cbranch_execz 1",
+      "v_mov_b32_e32 v3, v4", "s_or_b64 exec, exec, s[4:5]", "v_permlane16_swap_b32_e32 v1, v2",
+      "s_endpgm"], False),
+    # if / else: swap in the else arm flagged
+    (["v_cmp_gt_u32_e32 vcc, 16, v0", "s_and_saveexec_b64 s[4:5], vcc", "s_xor_b64 s[4:5], exec, s[4:5]",
+      "v_mov_b32_e32 v3, v4", "s_or_saveexec_b64 s[6:7], s[4:5]", "s_xor_b64 exec, exec, s[6:7]",
+      "v_permlane32_swap_b32_e32 v1, v2", "s_or_b64 exec, exec, s[6:7]", "s_endpgm"], True),
+    # a divergent loop: the swap after its exit is clean, one inside its body is flagged
+    (["s_mov_b64 s[8:9], 0", "v_add_u32_e32 v0, 1, v0", "v_cmp_le_u32_e32 vcc, 5, v0",
+      "s_or_b64 s[8:9], vcc, s[8:9]", "s_andn2_b64 exec, exec, s[8:9]", "s_cbranch_execnz 65531",
+      "s_or_b64 exec, exec, s[8:9]", "v_permlane16_swap_b32_e32 v1, v2", "s_endpgm"], False),
+    (["s_mov_b64 s[8:9], 0", "v_add_u32_e32 v0, 1, v0", "v_permlane16_swap_b32_e32 v1, v2",
+      "v_cmp_le_u32_e32 vcc, 5, v0", "s_or_b64 s[8:9], vcc, s[8:9]", "s_andn2_b64 exec, exec, s[8:9]",
+      "s_cbranch_execnz 65530", "s_or_b64 exec, exec, s[8:9]", "s_endpgm"], True),
+])
+def test_scan_flags_swaps_in_divergent_regions(lines, flag):
+    import exec_scan
+
+    (name, body), = list(exec_scan.functions(_fn(lines)))
+    assert bool(exec_scan.scan_function(body)) == flag

@@ -14,9 +14,9 @@ for L in "$@"; do
     --timeout-method thread > "$O/tests_$n.log" 2>&1 || { echo "TESTS FAILED $n"; tail -30 "$O/tests_$n.log"; exit 1; }
   echo "$n: $(tail -1 "$O/tests_$n.log")"
 done
-specs=()
-for L in "$@"; do specs+=("$L:4"); done
-bash tools/ab_bench.sh "${specs[@]}" | tee "$O/ab.log" || exit 1
+
+
+bash tools/ab_bench.sh "$@" | tee "$O/ab.log" || exit 1
 R=$(pwd)
 for L in "$@"; do
   n=$(basename "$L" .so)

@@ -33,7 +33,7 @@ def run(eng, xe, xd, out, host_idx, n=100):
 
 
 def main():
-    variants = [int(v) for v in sys.argv[1:]] or [3]
+    variants = [int(v) for v in sys.argv[1:]] or [4]
     dev = torch.device("cuda:0")
     m = bench.build_model(dev)
     eng = m.engine(dev)
