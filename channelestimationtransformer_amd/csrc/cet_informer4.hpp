@@ -141,7 +141,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       }
       if (sparse) io.cnt = CNT;
     }
-    attention_head<P, MQ_, MK_>(io, M, w);
+    attention_head<P, MQ_, MK_, false, true>(io, M, w);   // encoder (every nmt has its case) and decoder self-attention: exact
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
@@ -184,7 +184,9 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
           case 1: enc_attend(IC<1>{}); break;
           case 2: enc_attend(IC<2>{}); break;
           case 3: enc_attend(IC<3>{}); break;
-          default: enc_attend(IC<MT>{}); break;
+          case 4: enc_attend(IC<4>{}); break;
+          case 5: enc_attend(IC<5>{}); break;
+          default: enc_attend(IC<MT>{}); break;   // exactly MT tiles: every key-tile bound is exact
         }
       }
       const WPre<P, 4> po = prefetch_res<P, 4>(M, ELD.o);   // x = x + new_x (encoder.py:49)
@@ -343,12 +345,20 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       __syncthreads();
       STAMP();  // decoder self-attention
       gemm_res_n<P, 4, NMD>(po, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+#ifndef CET_NO_CROSSQ_PRE
+      // the cross-attention's Q weights of head w, requested before LN1's barrier (the decoder's residual
+      // is one tile: the registers are free here)
+      const WPre<P, 4> pcq = prefetch_res<P, 4>(M, cq);
+      const WPre<P, 4>* cqp = &pcq;
+#else
+      const WPre<P, 4>* cqp = nullptr;
+#endif
       ln_res(XD, nmd, Ld, M, DLD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
       __syncthreads();
       {
         // cross-attention: FullAttention over the encoder-stack output, mix=False
 #ifndef CET_NO_CROSS_HOIST
-        attention_head<P, NMD, NMS, true>(cio, M, w, CK, CV);
+        attention_head<P, NMD, NMS, true, NMS == 1>(cio, M, w, CK, CV, cqp);
 #else
         const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
         attend(IC<NMD>{}, IC<NMS>{}, XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),

@@ -103,6 +103,8 @@ __global__ void __launch_bounds__(NTHREADS, 4)
         case 1: go(TIC<1>{}); break;
         case 2: go(TIC<2>{}); break;
         case 3: go(TIC<3>{}); break;
+        case 4: go(TIC<4>{}); break;
+        case 5: go(TIC<5>{}); break;
         default: go(TIC<MT>{}); break;
       }
     }

@@ -567,9 +567,9 @@ __device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem&
 }
 
 // LayerNorm of the register residual over all 128 features (8 waves × 16).
-//   1. each wave reduces its 16 features per row to (mean_w, M2_w) and stores the pair (LDS partials);
-//   2. wave w < nmt combines the 8 pairs of the rows of m-tile w (Chan's combination: the exact row
-//      mean / variance) into (mean, 1/std) per row — once per row, not once per wave;
+//   1. each wave reduces its 16 features per row to (Σx, Σx²) and stores the pair (LDS partials);
+//   2. wave w < nmt combines the 8 pairs of the rows of m-tile w into (mean, 1/std) per row — once per
+//      row, not once per wave (-DCET_LN_TWOPASS: per-wave (mean, M2) and Chan's combination);
 //   3. every wave normalises its fragments from those row statistics.
 // Normalised rows go to X and rows < `rows` to the image `out` (and `out2`).  torch.nn.LayerNorm
 // (biased var, eps in the sqrt) or, if unbiased_std, the reference Transformer's LayerNormalization.
@@ -583,13 +583,59 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   const int nb = 16 * w + 4 * g;
   float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
   const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
+#ifndef CET_LN_TWOPASS
+  // One pass: each wave publishes (Σx, Σx²) over its 16 features per row.  The two butterflies share
+  // their swaps: permlane16_swap(s, q) leaves rows (s0+s1, q0+q1, s2+s3, q2+q3) after one add, and the
+  // 32-lane swap then gives Σs in rows 0 / 2 and Σq in rows 1 / 3 — lanes g and g + 2 store the same
+  // word to the same address, so the publish needs no branch.
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
-#ifdef CET_ABL_LN
-    if (false) {
-#else
     if (mt < nmt) {
+      const f32x4 x = X.v[mt];
+      const float s = (x[0] + x[1]) + (x[2] + x[3]);
+      const float q = fmaf(x[3], x[3], fmaf(x[2], x[2], fmaf(x[1], x[1], x[0] * x[0])));
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(q), false, false);
+      const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+      part[(mt * 16 + c) * LN_STRIDE + 2 * w + (g & 1)] = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+    }
+  }
+  __syncthreads();
+  // row statistics (mean, 1/std) of row m from the 8 waves' (Σx, Σx²)
+  auto row_stats = [&](int m) __attribute__((always_inline)) {
+    const float* pr = part + m * LN_STRIDE;
+    const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
+    const float sx = ((p0[0] + p0[2]) + (p1[0] + p1[2])) + ((p2[0] + p2[2]) + (p3[0] + p3[2]));
+    const float sq = ((p0[1] + p0[3]) + (p1[1] + p1[3])) + ((p2[1] + p2[3]) + (p3[1] + p3[3]));
+    const float mean = sx * (1.0f / 128.0f);
+    const float M2 = fmaxf(fmaf(-sx, mean, sq), 0.f);   // Σx² − (Σx)²/128
+    const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
+                                   : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
+    return f32x2{mean, inv};
+  };
+#ifndef CET_LN_TWO_BARRIER
+  if constexpr (N == 1) {
+    // one m-tile (the decoder's 15 rows): every wave combines its own rows' partials — no second
+    // barrier; the caller's barrier after the LN orders these reads before the partials are rewritten
+    if (nmt > 0) {
+      const f32x2 st = row_stats(c);
+      const f32x4 y = (X.v[0] - st[0]) * st[1] * g0 + b0;
+      if (INPLACE) X.v[0] = y;
+      if (c < rows) {
+        out.st4(c, nb, y);
+        if (out2) out2->st4(c, nb, y);
+      }
+    }
+    return;
+  }
 #endif
+  // wave w < nmt: the rows of m-tile w, once per row (every lane group stores the same pair)
+  if (w < nmt) *reinterpret_cast<f32x2*>(stats + 2 * (w * 16 + c)) = row_stats(w * 16 + c);
+#else
+  // two passes (mean, then Σ(x − mean)²) per wave, Chan's combination over the waves
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
       float s = (X.v[mt][0] + X.v[mt][1]) + (X.v[mt][2] + X.v[mt][3]);
       s = xor_sum(s, 16);
       s = xor_sum(s, 32);
@@ -606,11 +652,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     }
   }
   __syncthreads();
-#ifdef CET_ABL_LN
-  if (w < 0) {
-#else
   if (w < nmt) {
-#endif
     const int m = w * 16 + c;
     const float* pr = part + m * LN_STRIDE;
     const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
@@ -623,6 +665,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
                                    : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
     if (g == 0) *reinterpret_cast<f32x2*>(stats + 2 * m) = f32x2{mean, inv};
   }
+#endif
   __syncthreads();
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
@@ -836,10 +879,13 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, i
 }
 
 // EXTKV: the K/V tiles come from the caller (kin / vin, project_kv) instead of being projected here.
-template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false>
+// NKX: the caller guarantees ceil(LK / 16) == MK (the key-tile bound is exact).
+// qpre: the Q weight fragments and epilogue vectors of head h, requested by the caller ahead of time.
+template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false, bool NKX = false>
 __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
                                                const AF<plain_of<PD>()>* kin = nullptr,
-                                               const AF<plain_of<PD>()>* vin = nullptr) {
+                                               const AF<plain_of<PD>()>* vin = nullptr,
+                                               const WPre<PD, 4>* qpre = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -883,8 +929,15 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
   // Q tiles are projected where they are consumed (per query tile in M, per selected tile in the
   // softmax): wq and its epilogue vectors are the only Q state that lives
   if constexpr (!EARLYQ) {
-    load_frags<PD, 4>(m, io.wq, h, wq);
-    epi_vecs(m, io.dq, fq, sq, bq);
+    if (qpre) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) wq[ks] = qpre->a[ks];
+      sq = qpre->sc;
+      bq = qpre->bi;
+    } else {
+      load_frags<PD, 4>(m, io.wq, h, wq);
+      epi_vecs(m, io.dq, fq, sq, bq);
+    }
   }
   auto project_q = [&](int row) __attribute__((always_inline)) {
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
@@ -1015,42 +1068,53 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
   }
   SUB(4);
 
-  // ---- softmax(scale·q·Kᵀ [mask])·V for the selected queries (attn.py:109-138 / 57-65)
+  // ---- softmax(scale·q·Kᵀ [mask])·V for the selected queries (attn.py:109-138 / 57-65).  The mask
+  //      enters the score MFMA as its accumulator init (−inf on masked keys, 0 elsewhere), so neither
+  //      sweep selects per score: the max runs over the raw scores (scale = 2^-2 commutes with max
+  //      exactly) and exp(−inf) = 0 zeroes the masked probabilities.  Non-causal calls mask only keys
+  //      ≥ L_K, which lie in the last key tile (nkt == MK when NKX), computed once per call.
   const float scale = 0.25f;
   const int nsel = sparse ? io.u : LQ;
   const int nst = (nsel + 15) >> 4;
+  if constexpr (NKX) __builtin_assume(nkt == MK);
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  auto key_mask = [&](int kt, int lim) __attribute__((always_inline)) {   // keys ≥ lim → −inf
+    f32x4 z;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[r] = kt * 16 + g * 4 + r >= lim ? NEG_INF : 0.f;
+    return z;
+  };
+  const f32x4 last_mask = key_mask(nkt - 1, LK);
 #pragma unroll 1
   for (int st = 0; st < nst; ++st) {
     const int i = st * 16 + col;
     const int ic = i < nsel ? i : nsel - 1;
     const int qi = sparse ? (int)sel[ic] : ic;
     const AF<PA> qs = project_q(qi);
+    const int lim = io.causal ? (qi + 1 < LK ? qi + 1 : LK) : LK;   // the first masked key of this query
+    f32x4 init[MK];
+#pragma unroll
+    for (int kt = 0; kt < MK; ++kt) init[kt] = io.causal ? key_mask(kt, lim) : (kt == nkt - 1 ? last_mask : zero4);
     float mx = NEG_INF;
 #pragma unroll
     for (int kt = 0; kt < MK; ++kt) {
       if (kt < nkt) {
-        const f32x4 a = mma16<PA>(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kt * 16 + g * 4 + r;
-          const bool masked = key >= LK || (io.causal && key > qi);
-          mx = masked ? mx : fmaxf(mx, a[r] * scale);
-        }
+        const f32x4 a = mma16<PA>(Kf[kt], qs, init[kt]);
+        mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fmaxf(a[0], a[1]), __builtin_fmaxf(a[2], a[3])));
       }
     }
     mx = xor_max(mx, 16);
     mx = xor_max(mx, 32);
+    mx *= scale;
     float sum = 0.f;
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < MK; ++kt) {
       if (kt < nkt) {
-        f32x4 p = mma16<PA>(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
+        f32x4 p = mma16<PA>(Kf[kt], qs, init[kt]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kt * 16 + g * 4 + r;
-          const bool masked = key >= LK || (io.causal && key > qi);
-          p[r] = masked ? 0.f : __expf(p[r] * scale - mx);
+          p[r] = __expf(p[r] * scale - mx);
           sum += p[r];
         }
         o = mma16<PA>(Vf[kt], split4<PA>(p), o);
@@ -1066,12 +1130,11 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
 #pragma unroll
         for (int kt = 0; kt < MK; ++kt)
           if (kt < nkt) {
-            const f32x4 p = mma16<PA>(Kf[kt], qs, f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 p = mma16<PA>(Kf[kt], qs, init[kt]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int key = kt * 16 + g * 4 + r;
-              const bool masked = key >= LK || (io.causal && key > qi);
-              if (key < LK) arow[key] = masked ? 0.f : __expf(p[r] * scale - mx) * inv;
+              if (key < LK) arow[key] = __expf(p[r] * scale - mx) * inv;
             }
           }
       }
