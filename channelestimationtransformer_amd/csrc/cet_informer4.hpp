@@ -110,12 +110,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     io.st = nullptr;
     return io;
   };
-  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles
-  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
-                    uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
-                    int mix, int call, float* attn_out) {
-    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
-    HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
+  // the ProbSparse draws of one attention call: u, the multiplicity table (replayed in-kernel or staged)
+  auto call_setup = [&](HeadIO<P>& io, int call) __attribute__((always_inline)) {
     io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
     if (call >= 0) {
       const AttnCall& c = PL.calls[call];
@@ -141,7 +137,16 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       }
       if (sparse) io.cnt = CNT;
     }
-    attention_head<P, MQ_, MK_, false, true>(io, M, w);   // encoder (every nmt has its case) and decoder self-attention: exact
+  };
+  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles (exact: the encoder has
+  // a case for every nmt, the decoder self-attention's bound is its own length)
+  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
+                    uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
+                    int mix, int call, float* attn_out) {
+    constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
+    call_setup(io, call);
+    attention_head<P, MQ_, MK_, false, true>(io, M, w);
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {

@@ -842,24 +842,36 @@ struct HeadIO {
   unsigned long long* st;     // diagnostics: sub-phase s_memtime stamps of head 0, or nullptr
 };
 
+// The K and V weight fragments of head h and their epilogue vectors, requested ahead of their use.
+template <int PD>
+struct KVPre {
+  WF<PD> k[4], v[4];
+  f32x4 sk, bk;
+  float sv, bv;
+};
+template <int PD>
+__device__ __forceinline__ KVPre<PD> prefetch_kv(const HeadIO<PD>& io, const Mem& m, int h) {
+  KVPre<PD> p;
+  const int lane = lane_op();
+  const int col = lane & 15, g = lane >> 4;
+  load_frags<PD, 4>(m, io.wk, h, p.k);
+  load_frags<PD, 4>(m, io.wv, h, p.v);
+  epi_vecs(m, io.dk, 16 * h + 4 * g, p.sk, p.bk);
+  p.sv = io.dv.scale != NONE ? pload1(m, io.dv.scale, 16 * h + col) : 1.f;
+  p.bv = io.dv.bias != NONE ? pload1(m, io.dv.bias, 16 * h + col) : 0.f;
+  return p;
+}
+
 // K and V tiles of head h from the key/value rows (attn.py:195-199): Kᵀ = Wk_h·Xᵀ as the A fragments
 // of Sᵀ = K·Qᵀ, V = X·Wv_hᵀ as the A fragments of Oᵀ = Vᵀ·Pᵀ.
 template <int PD, int MK>
-__device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, int h, AF<plain_of<PD>()> (&Kf)[MK],
+__device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const KVPre<PD>& w, AF<plain_of<PD>()> (&Kf)[MK],
                                            AF<plain_of<PD>()> (&Vf)[MK]) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
-  const int col = lane & 15, g = lane >> 4;
+  const int col = lane & 15;
   const int nkt = (io.LK + 15) >> 4;
-  const int fq = 16 * h + 4 * g;
   const int kq = kq_of<PD>(lane);
-  WF<PD> wk[4], wv[4];
-  load_frags<PD, 4>(m, io.wk, h, wk);
-  load_frags<PD, 4>(m, io.wv, h, wv);
-  f32x4 sk, bk;
-  epi_vecs(m, io.dk, fq, sk, bk);
-  const float sv = io.dv.scale != NONE ? pload1(m, io.dv.scale, 16 * h + col) : 1.f;
-  const float bv = io.dv.bias != NONE ? pload1(m, io.dv.bias, 16 * h + col) : 0.f;
 #pragma unroll
   for (int mt = 0; mt < MK; ++mt) {
     Kf[mt] = AF<PA>{};
@@ -869,13 +881,18 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, i
 #pragma unroll
       for (int ks = 0; ks < 4; ks += KR<PD>) {
         const XF<PD> bx = io.xkv.ld(mt * 16 + col, ks * 32 + kq);
-        k = mma<PD>(&wk[ks], bx, k);
-        v = mma_xw<PD>(bx, &wv[ks], v);
+        k = mma<PD>(&w.k[ks], bx, k);
+        v = mma_xw<PD>(bx, &w.v[ks], v);
       }
-      Kf[mt] = split4<PA>(k * sk + bk);
-      Vf[mt] = split4<PA>(v * sv + bv);
+      Kf[mt] = split4<PA>(k * w.sk + w.bk);
+      Vf[mt] = split4<PA>(v * w.sv + w.bv);
     }
   }
+}
+template <int PD, int MK>
+__device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, int h, AF<plain_of<PD>()> (&Kf)[MK],
+                                           AF<plain_of<PD>()> (&Vf)[MK]) {
+  project_kv<PD, MK>(io, prefetch_kv<PD>(io, m, h), Kf, Vf);
 }
 
 // EXTKV: the K/V tiles come from the caller (kin / vin, project_kv) instead of being projected here.
@@ -965,17 +982,21 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
         if (kt < nkt) {
           const f32x4 s = mma16<PA>(Kf[kt], qf, f32x4{0.f, 0.f, 0.f, 0.f});
           const uint32_t cw = cws[kt];
+          f32x4 t;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
 #ifdef CET_ABL_MVALU
             sum += s[r]; (void)cw;   // ablation (wrong results)
-            mx = fmaxf(mx, s[r]);
+            t[r] = s[r];
 #else
             const float cf = (float)((cw >> (8 * r)) & 0xffu);
             sum = fmaf(cf, s[r], sum);
-            mx = fmaxf(mx, cf != 0.f ? s[r] : NEG_INF);
+            t[r] = cf != 0.f ? s[r] : NEG_INF;
 #endif
           }
+          // the sampled maximum, two keys per v_max3
+          mx = __builtin_fmaxf(mx, __builtin_fmaxf(t[0], t[1]));
+          mx = __builtin_fmaxf(mx, __builtin_fmaxf(t[2], t[3]));
         }
       }
       sum = xor_sum(sum, 16);
@@ -1043,28 +1064,20 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
   };
   if (sparse && !io.causal) {
     // ---- unselected rows keep the initial context, mean(V) (attn.py:116-119): written to every
-    //      row here, then the selected rows are overwritten below (same wave, LDS in order)
-    float part = 0.f;
+    //      row here, then the selected rows are overwritten below (same wave, LDS in order).  The key
+    //      sums come from the MFMA, Oᵀ = Vᵀ·I with I the indicator of the keys < L_K in every column:
+    //      lane (g, c) then holds features 4g .. 4g+3 and stores them 4-wide into rows c, c + 16, …
+    f32x4 vs = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < MK; ++kt)
-      if (kt < nkt)
+      if (kt < nkt) {
+        f32x4 ind;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v = (float)Vf[kt].h[j];
-          if constexpr (PA == P_X3) v += (float)Vf[kt].l[j];
-          part += (kt * 16 + g * 4 + j < LK) ? v : 0.f;
-        }
-    part = xor_sum(part, 16);
-    part = xor_sum(part, 32);
-    const float mean = part / (float)LK;
-    if (!io.mix) {
-      for (int q = g; q < LQ; q += 4) io.ctx.st1(q, h * 16 + col, mean);
-    } else {
-      for (int q = g; q < LQ; q += 4) {
-        const int f = h * LQ * 16 + q * 16 + col;
-        io.ctx.st1(f >> 7, f & 127, mean);
+        for (int j = 0; j < 4; ++j) ind[j] = kt * 16 + g * 4 + j < LK ? 1.f : 0.f;
+        vs = mma16<PA>(Vf[kt], split4<PA>(ind), vs);
       }
-    }
+    const f32x4 mean4 = vs * (1.0f / (float)LK);
+    for (int q = col; q < LQ; q += 16) ctx_st4(q, g * 4, mean4);
   }
   SUB(4);
 

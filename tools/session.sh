@@ -7,6 +7,7 @@
 #   prof       rocprofv3 --kernel-trace --stats over bench.py --inflight 1
 #   prof2      the same over the default bench.py
 #   pmcwait    SQ wait / issue breakdown (one PMC pass)   pmcinst  instruction counts (one PMC pass)
+#   pmcvalu    VALU instructions by kind (float add/mul/fma/transcendental, conversions, integer)
 #   traffic    FETCH_SIZE and WRITE_SIZE passes -> traffic.json
 #   stamps     DIAG per-phase stamps at B=512         configs  tools/bench_configs.py
 #   list       rocprofv3 -L (counter names)
@@ -46,11 +47,12 @@ for s in "$@"; do
         python "$R/bench.py" --no-cpu-baseline > "$R/$O/bench_under_rocprof.json" 2> "$R/$O/prof_if2.err") \
         || { tail -20 "$O/prof_if2.err"; exit 1; }
       find "$O/prof_if2" -name "*kernel_stats.csv" -exec cut -c1-220 {} \; | head -5 ;;
-    pmcwait|pmcinst|pmcmix)
+    pmcwait|pmcinst|pmcmix|pmcvalu)
       case $s in
         pmcwait) C="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" ;;
         pmcinst) C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT" ;;
         pmcmix) C="SQ_WAVES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_ACTIVE_INST_FLAT" ;;
+        pmcvalu) C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F SQ_INSTS_VALU_MUL_F SQ_INSTS_VALU_FMA_F SQ_INSTS_VALU_TRANS_F SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT" ;;
       esac
       (cd /tmp && $T 120 rocprofv3 --pmc $C --output-format csv -d "$R/$O/$s/p0" -o pmc -- $(fwd) > /dev/null \
         2> "$R/$O/$s.err") || { tail -20 "$O/$s.err"; exit 1; }
