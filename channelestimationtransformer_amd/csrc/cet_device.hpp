@@ -71,6 +71,12 @@ __device__ __forceinline__ bf16x4 cvt4(const f32x4& v) {
 // into EXEC-narrowed code (the retired two-sequence kernel, profiles/r03/bisect_*.txt).  Every call sits
 // at full EXEC in the source; tools/exec_scan.py checks the built code objects for a swap reached under
 // a narrowed EXEC (tests/test_isa_guard.py, CPU suite).
+// max of three as one v_max3_f32 (NaN-free operands; fmaxf trees get re-paired by the compiler)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ float swap_pair_sum16(float v) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);

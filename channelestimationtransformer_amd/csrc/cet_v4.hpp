@@ -592,8 +592,9 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
       const f32x4 x = X.v[mt];
-      const float s = (x[0] + x[1]) + (x[2] + x[3]);
-      const float q = fmaf(x[3], x[3], fmaf(x[2], x[2], fmaf(x[1], x[1], x[0] * x[0])));
+      // on the fragment's natural register pairs: packed math with no operand moves
+      const f32x2 hs = x.xy + x.zw, hq = x.xy * x.xy + x.zw * x.zw;
+      const float s = hs.x + hs.y, q = hq.x + hq.y;
       const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(q), false, false);
       const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
       const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
@@ -605,8 +606,9 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   auto row_stats = [&](int m) __attribute__((always_inline)) {
     const float* pr = part + m * LN_STRIDE;
     const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
-    const float sx = ((p0[0] + p0[2]) + (p1[0] + p1[2])) + ((p2[0] + p2[2]) + (p3[0] + p3[2]));
-    const float sq = ((p0[1] + p0[3]) + (p1[1] + p1[3])) + ((p2[1] + p2[3]) + (p3[1] + p3[3]));
+    // (Σx, Σx²) pairs summed as pairs (packed adds on the loaded register pairs)
+    const f32x2 t = ((p0.xy + p0.zw) + (p1.xy + p1.zw)) + ((p2.xy + p2.zw) + (p3.xy + p3.zw));
+    const float sx = t.x, sq = t.y;
     const float mean = sx * (1.0f / 128.0f);
     const float M2 = fmaxf(fmaf(-sx, mean, sq), 0.f);   // Σx² − (Σx)²/128
     const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
@@ -976,29 +978,29 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       const uint2* crow = reinterpret_cast<const uint2*>(io.cnt + (size_t)q * io.cnt_stride + g * 24);
       const uint2 c01 = crow[0], c23 = crow[1], c45 = crow[2];
       const uint32_t cws[MT] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
-      float sum = 0.f, mx = NEG_INF;
+      // Σ count·score as two packed chains; the sampled maximum through min(score, bound) with the
+      // bound count·2^64 − 2^63: ≥ 2^63 for a drawn key (the score passes), −2^63 for an undrawn one —
+      // below every score, and every query row holds U ≥ 1 draws, so the row maximum is a drawn score
+      constexpr float BND = 18446744073709551616.f, HALF = 9223372036854775808.f;
+      f32x2 sum2 = {0.f, 0.f};
+      float mx = -HALF;
 #pragma unroll
       for (int kt = 0; kt < MK; ++kt) {
         if (kt < nkt) {
           const f32x4 s = mma16<PA>(Kf[kt], qf, f32x4{0.f, 0.f, 0.f, 0.f});
           const uint32_t cw = cws[kt];
-          f32x4 t;
+          f32x4 cf;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-#ifdef CET_ABL_MVALU
-            sum += s[r]; (void)cw;   // ablation (wrong results)
-            t[r] = s[r];
-#else
-            const float cf = (float)((cw >> (8 * r)) & 0xffu);
-            sum = fmaf(cf, s[r], sum);
-            t[r] = cf != 0.f ? s[r] : NEG_INF;
-#endif
-          }
-          // the sampled maximum, two keys per v_max3
-          mx = __builtin_fmaxf(mx, __builtin_fmaxf(t[0], t[1]));
-          mx = __builtin_fmaxf(mx, __builtin_fmaxf(t[2], t[3]));
+          for (int r = 0; r < 4; ++r) cf[r] = (float)((cw >> (8 * r)) & 0xffu);
+          sum2 = cf.xy * s.xy + sum2;
+          sum2 = cf.zw * s.zw + sum2;
+          const f32x4 bnd = cf * BND - HALF;
+          // two keys per v_max3 (spelled out: the compiler re-pairs a max tree into three instructions)
+          mx = max3f(mx, __builtin_fminf(s[0], bnd[0]), __builtin_fminf(s[1], bnd[1]));
+          mx = max3f(mx, __builtin_fminf(s[2], bnd[2]), __builtin_fminf(s[3], bnd[3]));
         }
       }
+      float sum = sum2.x + sum2.y;
       sum = xor_sum(sum, 16);
       sum = xor_sum(sum, 32);
       mx = xor_max(mx, 16);
