@@ -58,15 +58,17 @@ __global__ void __launch_bounds__(NTHREADS, 4)
 
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;
   // full multi-head attention, one head per wave (no masks: the reference forward passes none)
-  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, const Img<P>& ctx, uint32_t Wq,
+  // NKXc: the key-tile bound MK is exact (ceil(LK / 16) == MK), so no key tile is skipped at run time
+  auto attend = [&](auto MQc, auto MKc, auto NKXc, const Img<P>& Xq, const Img<P>& Xkv, const Img<P>& ctx, uint32_t Wq,
                     uint32_t Wk, uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK) {
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    constexpr bool NKX_ = decltype(NKXc)::value;
     HeadIO<P> io;
     io.xq = Xq; io.xkv = Xkv; io.ctx = ctx; io.wq = Wq; io.wk = Wk; io.wv = Wv;
     io.dq = dq; io.dk = dk; io.dv = dv;
     io.LQ = LQ; io.LK = LK; io.prob = 0; io.causal = 0; io.mix = 0; io.u = LQ;
     io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = nullptr; io.m_dbg = nullptr; io.st = nullptr;
-    attention_head<P, MQ_, MK_>(io, M, w);
+    attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
   };
   auto part_of = [](GemmDesc d, int off) {
     if (d.bias != NONE) d.bias += off;
@@ -96,7 +98,7 @@ __global__ void __launch_bounds__(NTHREADS, 4)
     {
       const GemmDesc q = pl.enc[l].qkv;
       auto go = [&](auto NQ) __attribute__((always_inline)) {
-        attend(NQ, NQ, XB, XB, CTXI, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
+        attend(NQ, NQ, std::true_type{}, XB, XB, CTXI, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
                part_of(q, 128), part_of(q, 256), L, L);
       };
       switch (nmt) {
@@ -150,7 +152,7 @@ __global__ void __launch_bounds__(NTHREADS, 4)
       __syncthreads();
       {
         const GemmDesc q = dl.qkv;
-        attend(TIC<NMD>{}, TIC<NMD>{}, XBD, XBD, CTXD, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+        attend(TIC<NMD>{}, TIC<NMD>{}, std::false_type{}, XBD, XBD, CTXD, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
                part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld);
       }
       const WPre<P, 4> po = prefetch_res<P, 4>(M, dl.o);
@@ -161,7 +163,7 @@ __global__ void __launch_bounds__(NTHREADS, 4)
       __syncthreads();
       {
         const GemmDesc cq = dl.cq, ckv = dl.ckv;
-        attend(TIC<NMD>{}, TIC<MT>{}, XBD, ENC, CTXD, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+        attend(TIC<NMD>{}, TIC<MT>{}, std::false_type{}, XBD, ENC, CTXD, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
                part_of(ckv, 0), part_of(ckv, 128), Ld, L);
       }
       const WPre<P, 4> pco = prefetch_res<P, 4>(M, dl.co);

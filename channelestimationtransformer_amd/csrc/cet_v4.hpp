@@ -899,12 +899,14 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, i
 
 // EXTKV: the K/V tiles come from the caller (kin / vin, project_kv) instead of being projected here.
 // NKX: the caller guarantees ceil(LK / 16) == MK (the key-tile bound is exact).
-// qpre: the Q weight fragments and epilogue vectors of head h, requested by the caller ahead of time.
+// qpre / kvpre: the Q / K and V weight fragments and epilogue vectors of head h, requested by the
+// caller ahead of time.
 template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false, bool NKX = false>
 __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
                                                const AF<plain_of<PD>()>* kin = nullptr,
                                                const AF<plain_of<PD>()>* vin = nullptr,
-                                               const WPre<PD, 4>* qpre = nullptr) {
+                                               const WPre<PD, 4>* qpre = nullptr,
+                                               const KVPre<PD>* kvpre = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -941,6 +943,8 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       Kf[mt] = kin[mt];
       Vf[mt] = vin[mt];
     }
+  } else if (kvpre) {
+    project_kv<PD, MK>(io, *kvpre, Kf, Vf);
   } else {
     project_kv<PD, MK>(io, m, h, Kf, Vf);
   }
@@ -958,11 +962,11 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       epi_vecs(m, io.dq, fq, sq, bq);
     }
   }
-  auto project_q = [&](int row) __attribute__((always_inline)) {
+  auto project_q = [&](int row, float post = 1.f) __attribute__((always_inline)) {
     f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ks += KR<PD>) q = mma<PD>(&wq[ks], io.xq.ld(row, ks * 32 + kq), q);
-    return split4<PA>(q * sq + bq);
+    return split4<PA>(post == 1.f ? q * sq + bq : (q * sq + bq) * post);
   };
 
   SUB(2);
@@ -1085,10 +1089,9 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
 
   // ---- softmax(scale·q·Kᵀ [mask])·V for the selected queries (attn.py:109-138 / 57-65).  The mask
   //      enters the score MFMA as its accumulator init (−inf on masked keys, 0 elsewhere), so neither
-  //      sweep selects per score: the max runs over the raw scores (scale = 2^-2 commutes with max
-  //      exactly) and exp(−inf) = 0 zeroes the masked probabilities.  Non-causal calls mask only keys
+  //      sweep selects per score: the scores come out already scaled (2^-2 in the query operand) and
+  //      exp2(−inf) = 0 zeroes the masked probabilities.  Non-causal calls mask only keys
   //      ≥ L_K, which lie in the last key tile (nkt == MK when NKX), computed once per call.
-  const float scale = 0.25f;
   const int nsel = sparse ? io.u : LQ;
   const int nst = (nsel + 15) >> 4;
   if constexpr (NKX) __builtin_assume(nkt == MK);
@@ -1105,7 +1108,8 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
     const int i = st * 16 + col;
     const int ic = i < nsel ? i : nsel - 1;
     const int qi = sparse ? (int)sel[ic] : ic;
-    const AF<PA> qs = project_q(qi);
+    // the 1/√E = 2^-2 scale rides in the query operand (exact: a power of two)
+    const AF<PA> qs = project_q(qi, 0.25f);
     const int lim = io.causal ? (qi + 1 < LK ? qi + 1 : LK) : LK;   // the first masked key of this query
     f32x4 init[MK];
 #pragma unroll
@@ -1120,7 +1124,10 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
     }
     mx = xor_max(mx, 16);
     mx = xor_max(mx, 32);
-    mx *= scale;
+    // p = exp2(s·log2e − max·log2e) on the scaled scores: one FMA and one v_exp_f32 per score
+    constexpr float LOG2E = 1.4426950408889634f;
+    mx *= LOG2E;
+    auto prob = [&](float a) __attribute__((always_inline)) { return __builtin_amdgcn_exp2f(fmaf(a, LOG2E, -mx)); };
     float sum = 0.f;
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1129,7 +1136,7 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
         f32x4 p = mma16<PA>(Kf[kt], qs, init[kt]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          p[r] = __expf(p[r] * scale - mx);
+          p[r] = prob(p[r]);
           sum += p[r];
         }
         o = mma16<PA>(Vf[kt], split4<PA>(p), o);
@@ -1149,7 +1156,7 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int key = kt * 16 + g * 4 + r;
-              if (key < LK) arow[key] = __expf(p[r] * scale - mx) * inv;
+              if (key < LK) arow[key] = prob(p[r]) * inv;
             }
           }
       }
