@@ -72,18 +72,6 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       for (int j = 0; j < 4; ++j) lb4[j] = t4 + j < nlab ? lp[j] : 0.f;
     }
   }
-#ifdef CET_EMB_PRE
-  // the first encoder's embedding operands (weight fragments, epilogue vectors, positional rows) are
-  // requested with the inputs, so their L2/HBM latency overlaps the zeroing and the sampler load
-  const WPre<PP, 2> emb_w = prefetch_res<PP, 2>(M, PL.emb_enc);
-  f32x4 emb_pe[MT];
-  {
-    const int lane = lane_op();
-    const int n0 = 16 * w + (lane >> 4) * 4;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) emb_pe[mt] = pload4(M, PL.pe_enc, (mt * 16 + (lane & 15)) * DMODEL + n0);
-  }
-#endif
   // zero the activation images: rows past L are read (never used) by MFMAs
   for (int i = threadIdx.x; i < PL.lds4_zero / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -157,24 +145,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
                     int mix, int call, float* attn_out) {
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
-#if defined(CET_KV_EARLY) || defined(CET_KVQ_EARLY)
-    // the head's weight fragments are requested before the call's draws are replayed (barriers), so
-    // their L2 latency overlaps the replay
-    const KVPre<P> kvp = prefetch_kv<P>(io, M, w);
-#ifdef CET_KVQ_EARLY
-    WPre<P, 4> qp;
-    load_frags<P, 4>(M, io.wq, w, qp.a);
-    epi_vecs(M, io.dq, 16 * w + (lane_op() >> 4) * 4, qp.sc, qp.bi);
-    const WPre<P, 4>* qpp = &qp;
-#else
-    const WPre<P, 4>* qpp = nullptr;
-#endif
-    call_setup(io, call);
-    attention_head<P, MQ_, MK_, false, true>(io, M, w, nullptr, nullptr, qpp, &kvp);
-#else
     call_setup(io, call);
     attention_head<P, MQ_, MK_, false, true>(io, M, w);
-#endif
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
@@ -190,12 +162,6 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     for (int mt = 0; mt < MT; ++mt) X.v[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
       const GemmDesc d = PL.emb_enc;
-#ifdef CET_EMB_PRE
-      if (e == 0) {   // off == 0: positional rows mt·16 + c, all < LMAX
-        gemm_res<PP, 2, MT>(emb_w, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, 0},
-                            [&](int mt, int n0, f32x4 y) { X.v[mt] = y + emb_pe[mt]; });
-      } else
-#endif
       gemm_res<PP, 2, MT>(M, d, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, off}, [&](int mt, int n0, f32x4 y) {
         const int m = mt * 16 + (lane_op() & 15);
         const int prow = m + off < LMAX ? m + off : LMAX - 1;

@@ -79,10 +79,42 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // HBM instead of Y.  MT = ceil(L / 16) m-tiles, a compile-time count: the K loop is straight-line code
 // (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A reads of k ≥ K land
 // in the padded, finite part of the LDS image and meet zero weights.
+#ifdef LWF_INLINE
+#define LWF_GEMM_LINK __forceinline__
+#else
+#define LWF_GEMM_LINK __noinline__
+#endif
+#ifdef LWF_INLINE_ALL
+#define LWF_OP_LINK __forceinline__
+#else
+#define LWF_OP_LINK __noinline__
+#endif
+
+// A GEMM's first weight window and epilogue vectors for this wave's first n-tile, requested ahead (before
+// the barrier that precedes the GEMM), so their L2 latency overlaps the barrier wait
+struct FPre {
+  f32x4 wa[KW];
+  float sc, bi;
+};
+__device__ __forceinline__ FPre fpre(const float* __restrict__ blob, const float* __restrict__ pw, const FG g) {
+  FPre p;
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  const int N = uni(g.N), K = uni(g.K);
+  const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4;
+  const int nt = w < NT ? w : 0, n = 16 * nt + (lane & 15);
+  p.sc = uni(g.s) != (int)FNONE && n < N ? blob[g.s + n] : 1.f;
+  p.bi = uni(g.b) != (int)FNONE && n < N ? blob[g.b + n] : 0.f;
+  const f32x4* wp = reinterpret_cast<const f32x4*>(pw + g.w) + (size_t)nt * KQ * 64 + lane;
+#pragma unroll
+  for (int i = 0; i < KW; ++i) p.wa[i] = wp[(size_t)(i < KQ ? i : 0) * 64];
+  return p;
+}
+
 template <int AMODE, int MT>
-__device__ __noinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
+__device__ LWF_GEMM_LINK void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
                                      int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
-                                     int act, int res, float* __restrict__ gout, int t0, int ldo) {
+                                     int act, int res, float* __restrict__ gout, int t0, int ldo,
+                                     const FPre* pre = nullptr) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   const int r16 = lane & 15, q4 = lane >> 4;
   const int N = uni(g.N), K = uni(g.K);
@@ -108,9 +140,10 @@ __device__ __noinline__ void fgemm_t(const float* __restrict__ blob, const float
   }
   for (int nt = w; nt < NT; nt += 4) {
     const int n = 16 * nt + r16;
+    const bool first = pre && nt == w;
     // epilogue vectors requested before the K loop (their latency hides under the MFMAs)
-    const float sc = has_s && n < N ? blob[g.s + n] : 1.f;
-    const float bi = has_b && n < N ? blob[g.b + n] : 0.f;
+    const float sc = first ? pre->sc : has_s && n < N ? blob[g.s + n] : 1.f;
+    const float bi = first ? pre->bi : has_b && n < N ? blob[g.b + n] : 0.f;
     f32x4 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -118,7 +151,7 @@ __device__ __noinline__ void fgemm_t(const float* __restrict__ blob, const float
     // weights of KW k-quads in registers, the next window's loads in flight during this window's MFMAs
     f32x4 wa[KW], wb[KW];
 #pragma unroll
-    for (int i = 0; i < KW; ++i) wa[i] = wp[(size_t)(i < KQ ? i : 0) * 64];
+    for (int i = 0; i < KW; ++i) wa[i] = first ? pre->wa[i] : wp[(size_t)(i < KQ ? i : 0) * 64];
     for (int kc = 0; kc < KQ; kc += KW) {
 #pragma unroll
       for (int i = 0; i < KW; ++i) {
@@ -173,22 +206,28 @@ __device__ __noinline__ void fgemm_t(const float* __restrict__ blob, const float
 template <int AMODE>
 __device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g, int A,
                                       int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe, int act,
-                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
+                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0,
+                                      const FPre* pre = nullptr) {
   switch ((L + 15) >> 4) {
-    case 1: fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    case 2: fgemm_t<AMODE, 2>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    case 3: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    case 4: fgemm_t<AMODE, 4>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    case 5: fgemm_t<AMODE, 5>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    case 6: fgemm_t<AMODE, 6>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    case 7: fgemm_t<AMODE, 7>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
-    default: fgemm_t<AMODE, 8>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo); break;
+    case 1: fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+    case 2: fgemm_t<AMODE, 2>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+#ifdef LWF_INLINE
+    // inlined copies only for the plan's validated range (cet_lw_host.cpp build_fused: ≤ 48 rows)
+    default: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+#else
+    case 3: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+    case 4: fgemm_t<AMODE, 4>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+    case 5: fgemm_t<AMODE, 5>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+    case 6: fgemm_t<AMODE, 6>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+    case 7: fgemm_t<AMODE, 7>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+    default: fgemm_t<AMODE, 8>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
+#endif
   }
 }
 
 // LayerNorm of L rows of width D (eps 1e-5, biased variance; encoder.py:49-56), one wave per row; Y may
 // alias X.
-__device__ __noinline__ void fln(int X, int ldx, int L, int D, const float* __restrict__ g,
+__device__ LWF_OP_LINK void fln(int X, int ldx, int L, int D, const float* __restrict__ g,
                                  const float* __restrict__ bb, int Y, int ldy) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   X = uni(X); ldx = uni(ldx); L = uni(L); D = uni(D); Y = uni(Y); ldy = uni(ldy);
@@ -252,7 +291,7 @@ __device__ __noinline__ void fln(int X, int ldx, int L, int D, const float* __re
 // Q rows i at column h·E (stride ldq), K/V rows j; sparse: ProbSparse with the call's draws ix[LQ][U] and u;
 // causal: keys j > i masked (cumsum(V) as the initial context); mix: the (L, H, E) → (H, L, E) re-view of the
 // output (O dense [LQ][HE] at stride ldo).
-__device__ __noinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H, int E,
+__device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H, int E,
                                    int LQ, int LK, int causal, int mix, int sparse, int U, int u,
                                    const int32_t* __restrict__ ix, int scro) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
@@ -411,6 +450,14 @@ __device__ __noinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int
   }
 }
 
+#ifdef LWF_PRE_ON
+#define LWF_PRE(name, g) const FPre name = fpre(blob, pw, g)
+#define LWF_PP(name) &name
+#else
+#define LWF_PRE(name, g)
+#define LWF_PP(name) nullptr
+#endif
+
 #ifdef LWF_STAMPS
 // diagnostic build: cycles of workgroup 0 per category (0 GEMM, 1 attention, 2 LayerNorm, 3 other), printed
 #define LWF_ST_DECL uint64_t st_acc[4] = {0, 0, 0, 0}; uint64_t st_prev = __builtin_amdgcn_s_memtime();
@@ -477,18 +524,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
         fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
               u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
       }
+      LWF_PRE(po, ly->o);
       __syncthreads();
       LWF_ST(1)
-      fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
+      fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(po));   // x + attention (encoder.py:44-49)
       __syncthreads();
       LWF_ST(0)
       fln(X, ldD, L, D, blob + ly->g1, blob + ly->b1, X, ldD);
+      LWF_PRE(pf1, ly->f1);
       __syncthreads();
       LWF_ST(2)
-      fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
+      fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0, nullptr, 0, 0, LWF_PP(pf1));
+      LWF_PRE(pf2, ly->f2);
       __syncthreads();
       LWF_ST(0)
-      fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
+      fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(pf2));
       __syncthreads();
       LWF_ST(0)
       fln(X, ldD, L, D, blob + ly->g2, blob + ly->b2, X, ldD);
@@ -544,9 +594,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
       fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
             call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
     }
+    LWF_PRE(po, ly->o);
     __syncthreads();
     LWF_ST(1)
-    fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
+    fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(po));   // norm1(x + self-attention)
     __syncthreads();
     LWF_ST(0)
     fln(XD, ldD, Ld, D, blob + ly->g1, blob + ly->b1, XD, ldD);
@@ -557,18 +608,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
     __syncthreads();
     LWF_ST(0)
     fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr);
+    LWF_PRE(pco, ly->co);
     __syncthreads();
     LWF_ST(1)
-    fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
+    fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(pco));   // norm2(x + cross-attention)
     __syncthreads();
     LWF_ST(0)
     fln(XD, ldD, Ld, D, blob + ly->g2, blob + ly->b2, XD, ldD);
+    LWF_PRE(pf1, ly->f1);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
+    fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0, nullptr, 0, 0, LWF_PP(pf1));
+    LWF_PRE(pf2, ly->f2);
     __syncthreads();
     LWF_ST(0)
-    fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
+    fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(pf2));   // norm3(x + y)
     __syncthreads();
     LWF_ST(0)
     fln(XD, ldD, Ld, D, blob + ly->g3, blob + ly->b3, XD, ldD);

@@ -899,14 +899,12 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const Mem& m, i
 
 // EXTKV: the K/V tiles come from the caller (kin / vin, project_kv) instead of being projected here.
 // NKX: the caller guarantees ceil(LK / 16) == MK (the key-tile bound is exact).
-// qpre / kvpre: the Q / K and V weight fragments and epilogue vectors of head h, requested by the
-// caller ahead of time.
+// qpre: the Q weight fragments and epilogue vectors of head h, requested by the caller ahead of time.
 template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false, bool NKX = false>
 __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
                                                const AF<plain_of<PD>()>* kin = nullptr,
                                                const AF<plain_of<PD>()>* vin = nullptr,
-                                               const WPre<PD, 4>* qpre = nullptr,
-                                               const KVPre<PD>* kvpre = nullptr) {
+                                               const WPre<PD, 4>* qpre = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -943,8 +941,6 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       Kf[mt] = kin[mt];
       Vf[mt] = vin[mt];
     }
-  } else if (kvpre) {
-    project_kv<PD, MK>(io, *kvpre, Kf, Vf);
   } else {
     project_kv<PD, MK>(io, m, h, Kf, Vf);
   }
