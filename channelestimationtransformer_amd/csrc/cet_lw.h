@@ -108,14 +108,15 @@ struct FPlan {
   int call_U[F_MAX_CALLS], call_u[F_MAX_CALLS];
   uint32_t call_off[F_MAX_CALLS];
   // LDS layout (float offsets) and row strides
-  int oE0, oX, oT, oCTX, oENC, oXD, oSCR, scr_floats, lds_floats;
+  int oE1, e1_rows, oX, oT, oCTX, oENC, oXD, oSCR, scr_floats, lds_floats;   // E1: later stack windows' rows
+  int attn_waves;   // 8, or 4 when eight attention scratches would not fit (cet_lw_host.cpp build_fused)
   int ldD, ldT, ldH, ldF, ldKV, ldIN, ldINd;
   FEnc enc[F_MAX_ENC][F_MAX_EL];
   FDec dec[F_MAX_DEC];
 };
-int launch_fused(const FPlan* d_plan, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
+int launch_fused(const FPlan* d_plan, int D, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
                  const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st);
-int prepare_fused();
+int prepare_fused(int D);
 
 // ------------------------------------------------------------------ host model (cet_lw_host.cpp)
 // Weights as fp32 [N][K] matrices in one device blob (float offsets below); ProbSparse draws of a

@@ -74,11 +74,14 @@ int Model::build_fused() {
   p.dff = dff; p.S = S; p.prob = prob; p.mix = mix; p.act = act; p.stack = stack; p.nenc = nenc; p.ndec = ndec;
   p.ldD = pad(D); p.ldT = pad(3 * HE); p.ldH = pad(HE); p.ldF = pad(std::max(dff, D)); p.ldKV = pad(2 * HE);
   p.ldIN = C | 1; p.ldINd = Cd | 1;
-  const size_t nE0 = stack ? (size_t)r16(L0) * p.ldD : 0, nX = (size_t)r16(L0) * p.ldD;
+  // E1: the rows of the later encoders' windows x[:, -L0/2:] (each later window is a suffix of it)
+  p.e1_rows = stack && nenc >= 2 ? enc_L0[1] : 0;
+  const size_t nE1 = (size_t)p.e1_rows * p.ldD, nX = (size_t)r16(L0) * p.ldD;
   const size_t nT = std::max({(size_t)r16(Lm) * p.ldT, (size_t)r16(Ld) * p.ldH + (size_t)r16(S) * p.ldKV,
                               (size_t)r16(Lm) * p.ldF, (size_t)r16(L0) * p.ldIN, (size_t)r16(Ld) * p.ldINd});
   const size_t nCTX = (size_t)r16(Lm) * p.ldH, nENC = (size_t)r16(S) * p.ldD, nXD = (size_t)r16(Ld) * p.ldD;
-  auto scr_of = [&](int LQ, int LK) { return (size_t)r16(LQ) * (r16(LK) + 1) + 3 * (size_t)r16(LQ); };
+  // one head's scores (LQ rows of LK + 1 floats), M, sel and flag (cet_lwf.hip fattn)
+  auto scr_of = [&](int LQ, int LK) { return (size_t)LQ * (LK + 1) + 3 * (size_t)r16(LQ); };
   size_t scr = std::max({scr_of(L0, L0), scr_of(Ld, Ld), scr_of(Ld, S)});
   scr = (scr + 3) & ~(size_t)3;
   size_t o = 0;
@@ -87,12 +90,18 @@ int Model::build_fused() {
     o += (n + 3) & ~(size_t)3;
     return (int)at;
   };
-  p.oE0 = place(nE0); p.oX = place(nX); p.oT = place(nT); p.oCTX = place(nCTX); p.oENC = place(nENC);
-  p.oXD = place(nXD); p.oSCR = place(4 * scr);
+  p.oE1 = place(nE1); p.oX = place(nX); p.oT = place(nT); p.oCTX = place(nCTX); p.oENC = place(nENC);
+  p.oXD = place(nXD);
+  // attention on all 8 waves (one scratch each) unless only 4 scratches keep two workgroups per CU (80 KB)
+  // or keep the workgroup within the CU's 160 KB at all
+  const size_t base = o;
+  auto fits = [&](int aw, size_t kb) { return (base + aw * scr) * sizeof(float) <= kb * 1024; };
+  p.attn_waves = fits(8, 80) || (!fits(4, 80) && fits(8, 160)) ? 8 : 4;
+  p.oSCR = place(p.attn_waves * scr);
   p.scr_floats = (int)scr;
   p.lds_floats = (int)o;
   fused_lds = o * sizeof(float);
-  if (why) fprintf(stderr, "lw fused: lds %zu bytes\n", fused_lds);
+  if (why) fprintf(stderr, "lw fused: lds %zu bytes, attention on %d waves\n", fused_lds, p.attn_waves);
   if (fused_lds > 160 * 1024) return 0;
   // packed weights: Wp[nt][kq][lane][j] = W[16nt + (lane & 15)][16kq + 4j + (lane >> 4)]
   pblob.clear();
@@ -154,7 +163,7 @@ int Model::build_fused() {
   if (hipMalloc((void**)&d_pblob, pblob.size() * sizeof(float)) != hipSuccess) return -1;
   if (hipMemcpy(d_pblob, pblob.data(), pblob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (hipMemcpy(d_fplan, &p, sizeof(FPlan), hipMemcpyHostToDevice) != hipSuccess) return -1;
-  if (prepare_fused()) return -1;
+  if (prepare_fused(D)) return -1;
   fused_ok = true;
   return 0;
 }
@@ -208,7 +217,7 @@ int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, fl
                    hipStream_t st) {
   // the fused form: one launch, no workspace, no staging copies
   last_fused = fused_ok && use_fused && !(attns && out_attn);
-  if (last_fused) return launch_fused(d_fplan, fused_lds, d_blob, d_pblob, x_enc, x_dec, out, idx_dev, B, st);
+  if (last_fused) return launch_fused(d_fplan, D, fused_lds, d_blob, d_pblob, x_enc, x_dec, out, idx_dev, B, st);
   if (ensure_ws(B)) return -1;
   if (attns && out_attn) return enqueue(x_enc, x_dec, B, out, attns, idx_dev, st);
   const Key key{x_enc, x_dec, out, idx_dev, B};

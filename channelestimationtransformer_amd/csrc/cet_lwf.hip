@@ -1,5 +1,5 @@
 // Fused layer-wise forward (cet_lw.h FPlan): the InformerStack / Informer forward of one sequence per
-// 256-thread workgroup, every activation resident in LDS, for models whose per-sequence working set fits
+// 512-thread workgroup, every activation resident in LDS, for models whose per-sequence working set fits
 // (the MimoSimulation checkpoint architecture: d_model 64, seq_len 25, e_layers [4,3]).  It runs the same
 // operator sequence as the layer-wise launches (cet_lw_host.cpp Model::enqueue) in one launch:
 //   DataEmbedding (embed.py:118-135)              circular k=3 conv GEMM + pe rows
@@ -8,15 +8,17 @@
 //   ConvLayer (encoder.py:6-28)                   circular conv GEMM with folded BN, ELU, MaxPool(3,2,1)
 //   DecoderLayer (decoder.py:6-41)                causal self-attention (+ mix), cross-attention, FFN
 //   projection (model.py:264)                     the last pred_len rows straight to HBM
-//   ProbAttention / FullAttention (attn.py:37-175) per (head, wave) with the call's draws from HBM
+//   ProbAttention / FullAttention (attn.py:37-175) one head per wave with the call's draws from HBM
 // Arithmetic class: fp32 operands on v_mfma_f32_16x16x4_f32, as the layer-wise engine.
 //
-// Layout: wave w computes the 16-column n-tiles w, w + 4, … of a GEMM over every m-tile of the sequence
-// (one weight fragment feeds up to 8 m-tiles); its weights are a coalesced f32x4 per lane per 16 k
-// (host-packed, FPlan comment), the A operand is read from the LDS image; LDS row strides are ≡ 2 mod 32
-// floats (lanes 0-15 and 16-31 of an A read hit 32 distinct banks).  Attention: wave w owns heads w,
-// w + 4, …; scores, ProbSparse M, rank top-u and P live in the wave's own LDS scratch, no workgroup
-// barrier inside.
+// Layout: eight waves.  A GEMM's work is (n-tile, m-tile group) tasks: with two m-tiles (17-32 rows) wave w
+// takes m-tile w / 4 and the n-tiles w % 4, w % 4 + 4, …; otherwise every m-tile and the n-tiles w, w + 8, ….
+// Its weights are a coalesced f32x4 per lane per 16 k (host-packed, FPlan comment), the A operand is read
+// from the LDS image; LDS row strides are ≡ 2 mod 32 floats (lanes 0-15 and 16-31 of an A read hit 32
+// distinct banks).  Attention: wave w owns heads w, w + 8, … (w, w + 4, … on waves 0-3 when eight scratches
+// do not fit the plan's LDS); scores (LQ rows of LK + 1), ProbSparse M, rank top-u and P live in the wave's
+// own LDS scratch, no workgroup barrier inside.  The GEMMs, LayerNorm and attention are inlined into the
+// kernel body (no call ABI, no callee-saved spills).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,6 +34,8 @@ namespace lw {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+constexpr int NW = 8;              // waves per workgroup
+constexpr int NTH = NW * 64;       // threads per workgroup
 constexpr int KW = 4;              // k-quads (16 k each) of weights per register window
 
 __device__ __forceinline__ float fgelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
@@ -45,8 +49,7 @@ __device__ __forceinline__ float act_of(float y, int act) {
 
 extern __shared__ __attribute__((aligned(16))) float lsm[];   // the workgroup's LDS (dynamic size)
 
-// Sum over the 64 lanes, every lane gets it: quad permutes, row half-mirror and mirror (DPP), then the
-// 16- and 32-lane swaps (gfx950 v_permlane16/32_swap) — VALU only, no LDS round trip.
+// Sum over the 16 lanes of each DPP row: quad permutes, row half-mirror and mirror
 __device__ __forceinline__ float dpp_f(float v, int ctrl) {
   switch (ctrl) {
     case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
@@ -61,71 +64,31 @@ __device__ __forceinline__ float row16_sum(float v) {   // over the 16 lanes of 
   v += dpp_f(v, 0x141);
   return v + dpp_f(v, 0x140);
 }
-__device__ __forceinline__ float wave_sum(float v) {
-  v += dpp_f(v, 0xB1);    // quad_perm [1,0,3,2]
-  v += dpp_f(v, 0x4E);    // quad_perm [2,3,0,1]
-  v += dpp_f(v, 0x141);   // row_half_mirror: lane i of 8 with lane 7 − i
-  v += dpp_f(v, 0x140);   // row_mirror: lane i of 16 with lane 15 − i
-  v = swap_pair_sum16(v);
-  return swap_pair_sum32(v);
-}
 
 // A value every lane holds the same copy of, made provably uniform (scalar registers, scalar branches)
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Y[t][n] = act(Σ_k A(t, k)·W[n][k] · scale[n] + bias[n] + pe[t][n]) (+ Y[t][n] if res), t < L, n < N.
-// A and Y are LDS float offsets.  AMODE 0: A(t, k) = A[t·lda + k]; AMODE 1: circular k=3 conv,
-// A(t, tap·Cin + c) = A[((t − 1 + tap) mod L)·lda + c].  gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in
-// HBM instead of Y.  MT = ceil(L / 16) m-tiles, a compile-time count: the K loop is straight-line code
-// (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A reads of k ≥ K land
-// in the padded, finite part of the LDS image and meet zero weights.
-#ifdef LWF_INLINE
-#define LWF_GEMM_LINK __forceinline__
-#else
-#define LWF_GEMM_LINK __noinline__
-#endif
-#ifdef LWF_INLINE_ALL
-#define LWF_OP_LINK __forceinline__
-#else
-#define LWF_OP_LINK __noinline__
-#endif
-
-// A GEMM's first weight window and epilogue vectors for this wave's first n-tile, requested ahead (before
-// the barrier that precedes the GEMM), so their L2 latency overlaps the barrier wait
-struct FPre {
-  f32x4 wa[KW];
-  float sc, bi;
-};
-__device__ __forceinline__ FPre fpre(const float* __restrict__ blob, const float* __restrict__ pw, const FG g) {
-  FPre p;
-  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
-  const int N = uni(g.N), K = uni(g.K);
-  const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4;
-  const int nt = w < NT ? w : 0, n = 16 * nt + (lane & 15);
-  p.sc = uni(g.s) != (int)FNONE && n < N ? blob[g.s + n] : 1.f;
-  p.bi = uni(g.b) != (int)FNONE && n < N ? blob[g.b + n] : 0.f;
-  const f32x4* wp = reinterpret_cast<const f32x4*>(pw + g.w) + (size_t)nt * KQ * 64 + lane;
-#pragma unroll
-  for (int i = 0; i < KW; ++i) p.wa[i] = wp[(size_t)(i < KQ ? i : 0) * 64];
-  return p;
-}
-
+// Y[t][n] = act(Σ_k A(t, k)·W[n][k] · scale[n] + bias[n] + pe[t][n]) (+ Y[t][n] if res), t < L, n < N, over
+// the MT m-tiles m0, m0 + 1, … and the n-tiles n0, n0 + nstep, ….  A and Y are LDS float offsets.  AMODE 0:
+// A(t, k) = A[t·lda + k]; AMODE 1: circular k=3 conv, A(t, tap·Cin + c) = A[((t − 1 + tap) mod L)·lda + c].
+// gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in HBM instead of Y.  MT is compile-time, so the K loop is
+// straight-line code (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A
+// reads of k ≥ K land in the padded, finite part of the LDS image and meet zero weights.
 template <int AMODE, int MT>
-__device__ LWF_GEMM_LINK void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
-                                     int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
-                                     int act, int res, float* __restrict__ gout, int t0, int ldo,
-                                     const FPre* pre = nullptr) {
-  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+__device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
+                                        int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
+                                        int act, int res, float* __restrict__ gout, int t0, int ldo, int m0, int n0,
+                                        int nstep) {
+  const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, q4 = lane >> 4;
   const int N = uni(g.N), K = uni(g.K);
-  A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
   const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4;
   const bool has_b = uni(g.b) != (int)FNONE, has_s = uni(g.s) != (int)FNONE;
   // the lane's A rows (AMODE 0) / its three circular source rows per m-tile (AMODE 1)
   int rowoff[MT][3];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    int t = 16 * m + r16;
+    int t = 16 * (m0 + m) + r16;
     if (AMODE) {
       t = t < L ? t : L - 1;
 #pragma unroll
@@ -138,12 +101,11 @@ __device__ LWF_GEMM_LINK void fgemm_t(const float* __restrict__ blob, const floa
       rowoff[m][0] = rowoff[m][1] = rowoff[m][2] = A + t * lda;
     }
   }
-  for (int nt = w; nt < NT; nt += 4) {
+  for (int nt = n0; nt < NT; nt += nstep) {
     const int n = 16 * nt + r16;
-    const bool first = pre && nt == w;
     // epilogue vectors requested before the K loop (their latency hides under the MFMAs)
-    const float sc = first ? pre->sc : has_s && n < N ? blob[g.s + n] : 1.f;
-    const float bi = first ? pre->bi : has_b && n < N ? blob[g.b + n] : 0.f;
+    const float sc = has_s && n < N ? blob[g.s + n] : 1.f;
+    const float bi = has_b && n < N ? blob[g.b + n] : 0.f;
     f32x4 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -151,7 +113,7 @@ __device__ LWF_GEMM_LINK void fgemm_t(const float* __restrict__ blob, const floa
     // weights of KW k-quads in registers, the next window's loads in flight during this window's MFMAs
     f32x4 wa[KW], wb[KW];
 #pragma unroll
-    for (int i = 0; i < KW; ++i) wa[i] = first ? pre->wa[i] : wp[(size_t)(i < KQ ? i : 0) * 64];
+    for (int i = 0; i < KW; ++i) wa[i] = wp[(size_t)(i < KQ ? i : 0) * 64];
     for (int kc = 0; kc < KQ; kc += KW) {
 #pragma unroll
       for (int i = 0; i < KW; ++i) {
@@ -187,7 +149,7 @@ __device__ LWF_GEMM_LINK void fgemm_t(const float* __restrict__ blob, const floa
     for (int m = 0; m < MT; ++m) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int t = 16 * m + 4 * q4 + r;
+        const int t = 16 * (m0 + m) + 4 * q4 + r;
         if (t >= L) continue;
         float y = acc[m][r] * sc + bi;
         if (pe) y += pe[t * N + n];
@@ -203,98 +165,81 @@ __device__ LWF_GEMM_LINK void fgemm_t(const float* __restrict__ blob, const floa
   }
 }
 
+// The GEMM's task split over the eight waves (≤ 48 rows: the plan's validated range, cet_lw_host.cpp
+// build_fused): two m-tiles are split between the wave halves, one or three stay whole per wave.
 template <int AMODE>
 __device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g, int A,
                                       int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe, int act,
-                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0,
-                                      const FPre* pre = nullptr) {
+                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
+  const int w = uni(threadIdx.x >> 6);
+  A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
   switch ((L + 15) >> 4) {
-    case 1: fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-    case 2: fgemm_t<AMODE, 2>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-#ifdef LWF_INLINE
-    // inlined copies only for the plan's validated range (cet_lw_host.cpp build_fused: ≤ 48 rows)
-    default: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-#else
-    case 3: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-    case 4: fgemm_t<AMODE, 4>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-    case 5: fgemm_t<AMODE, 5>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-    case 6: fgemm_t<AMODE, 6>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-    case 7: fgemm_t<AMODE, 7>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-    default: fgemm_t<AMODE, 8>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, pre); break;
-#endif
+    case 1: fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    case 2:
+      fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, w / (NW / 2), w % (NW / 2),
+                        NW / 2);
+      break;
+    default: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
   }
 }
 
-// LayerNorm of L rows of width D (eps 1e-5, biased variance; encoder.py:49-56), one wave per row; Y may
-// alias X.
-__device__ LWF_OP_LINK void fln(int X, int ldx, int L, int D, const float* __restrict__ g,
-                                 const float* __restrict__ bb, int Y, int ldy) {
+// LayerNorm of L rows of width D ≤ 16·NC (eps 1e-5, biased variance; encoder.py:49-56): four rows per wave at
+// a time, 16 lanes per row; Y may alias X.
+template <int NC>
+__device__ __forceinline__ void fln(int X, int ldx, int L, int D, const float* __restrict__ g,
+                                    const float* __restrict__ bb, int Y, int ldy) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   X = uni(X); ldx = uni(ldx); L = uni(L); D = uni(D); Y = uni(Y); ldy = uni(ldy);
-  if (D <= 256) {   // four rows per wave at a time, 16 lanes per row
-    const int r16 = lane & 15, sub = lane >> 4;
-    float gv[16], bv[16];
+  const int r16 = lane & 15, sub = lane >> 4;
+  const float invD = 1.0f / (float)D;
+  float gv[NC], bv[NC];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = r16 + 16 * i;
-      gv[i] = c < D ? g[c] : 0.f;
-      bv[i] = c < D ? bb[c] : 0.f;
-    }
-    for (int t0 = 4 * w; t0 < L; t0 += 16) {
-      const int t = t0 + sub;
-      const bool on = t < L;
-      const int x = X + (on ? t : t0) * ldx;
-      float v[16];
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int c = r16 + 16 * i;
-        v[i] = c < D ? lsm[x + c] : 0.f;
-        s += v[i];
-      }
-      const float mean = row16_sum(s) / (float)D;
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float d = r16 + 16 * i < D ? v[i] - mean : 0.f;
-        q = fmaf(d, d, q);
-      }
-      const float inv = 1.0f / sqrtf(row16_sum(q) / (float)D + 1e-5f);
-      if (on) {
-        const int y = Y + t * ldy;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int c = r16 + 16 * i;
-          if (c < D) lsm[y + c] = (v[i] - mean) * inv * gv[i] + bv[i];
-        }
-      }
-    }
-    return;
+  for (int i = 0; i < NC; ++i) {
+    const int c = r16 + 16 * i;
+    gv[i] = c < D ? g[c] : 0.f;
+    bv[i] = c < D ? bb[c] : 0.f;
   }
-  for (int t = w; t < L; t += 4) {   // one row per wave
-    const int x = X + t * ldx;
+  for (int t0 = 4 * w; t0 < L; t0 += 4 * NW) {
+    const int t = t0 + sub;
+    const bool on = t < L;
+    const int x = X + (on ? t : t0) * ldx;
+    float v[NC];
     float s = 0.f;
-    for (int c = lane; c < D; c += 64) s += lsm[x + c];
-    const float mean = wave_sum(s) / (float)D;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = r16 + 16 * i;
+      v[i] = c < D ? lsm[x + c] : 0.f;
+      s += v[i];
+    }
+    const float mean = row16_sum(s) * invD;
     float q = 0.f;
-    for (int c = lane; c < D; c += 64) {
-      const float d = lsm[x + c] - mean;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const float d = r16 + 16 * i < D ? v[i] - mean : 0.f;
       q = fmaf(d, d, q);
     }
-    const float inv = 1.0f / sqrtf(wave_sum(q) / (float)D + 1e-5f);
-    const int y = Y + t * ldy;
-    for (int c = lane; c < D; c += 64) lsm[y + c] = (lsm[x + c] - mean) * inv * g[c] + bb[c];
+    const float inv = 1.0f / sqrtf(row16_sum(q) * invD + 1e-5f);
+    if (on) {
+      const int y = Y + t * ldy;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const int c = r16 + 16 * i;
+        if (c < D) lsm[y + c] = (v[i] - mean) * inv * gv[i] + bv[i];
+      }
+    }
   }
 }
 
-// Attention of one sequence (attn.py:37-175; the semantics of lw_attention): wave w takes heads w, w + 4, …
+// Attention of one sequence (attn.py:37-175; the semantics of lw_attention): wave w < AW takes heads w, w + AW, …
 // Q rows i at column h·E (stride ldq), K/V rows j; sparse: ProbSparse with the call's draws ix[LQ][U] and u;
 // causal: keys j > i masked (cumsum(V) as the initial context); mix: the (L, H, E) → (H, L, E) re-view of the
-// output (O dense [LQ][HE] at stride ldo).
-__device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H, int E,
-                                   int LQ, int LK, int causal, int mix, int sparse, int U, int u,
-                                   const int32_t* __restrict__ ix, int scro) {
+// output (O dense [LQ][HE] at stride ldo).  The wave's scratch holds S as LQ rows of LK + 1 floats (stores of
+// rows ≥ LQ and keys ≥ LK are skipped; P·V reads keys ≥ LK as zero), then M, sel and flag.
+__device__ __forceinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H, int E,
+                                      int LQ, int LK, int causal, int mix, int sparse, int U, int u,
+                                      const int32_t* __restrict__ ix, int scro, int AW) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  AW = uni(AW);
   Qo = uni(Qo); ldq = uni(ldq); Ko = uni(Ko); ldk = uni(ldk); Vo = uni(Vo); ldv = uni(ldv); Oo = uni(Oo);
   ldo = uni(ldo); H = uni(H); E = uni(E); LQ = uni(LQ); LK = uni(LK); causal = uni(causal); mix = uni(mix);
   sparse = uni(sparse); U = uni(U); u = uni(u); scro = uni(scro);
@@ -304,15 +249,15 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
   float* O = lsm + Oo;
   float* scr = lsm + scro;
   const int r16 = lane & 15, q4 = lane >> 4;
-  const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15, SS = LKp + 1;
+  const int LQp = (LQ + 15) & ~15, LKp = (LK + 15) & ~15, SS = LK + 1;
   const int HE = H * E;
   float* S = scr;
-  float* Mv = S + LQp * SS;
+  float* Mv = S + LQ * SS;
   int* sel = reinterpret_cast<int*>(Mv + LQp);
   int* flag = sel + LQp;
   const float scale = 1.0f / sqrtf((float)E);
   const int nqt = LQp >> 4, nkt = LKp >> 4, Ep = (E + 3) & ~3;
-  for (int h = w; h < H; h += 4) {
+  for (int h = w < AW ? w : H; h < H; h += AW) {
     const int hc = h * E;
     auto store = [&](int q, int e, float v) {
       if (!mix) {
@@ -322,7 +267,7 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
         O[row * ldo + (f - row * HE)] = v;
       }
     };
-    // ---- S = Q_h · K_hᵀ (unscaled)
+    // ---- S = Q_h · K_hᵀ (unscaled), rows < LQ and keys < LK
     for (int tt = 0; tt < nqt * nkt; ++tt) {
       const int qt = tt / nkt, kt = tt - qt * nkt;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -332,8 +277,12 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
         const float b = e < E ? K[(16 * kt + r16) * ldk + hc + e] : 0.f;
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
       }
+      const int key = 16 * kt + r16;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) S[(16 * qt + 4 * q4 + r) * SS + 16 * kt + r16] = acc[r];
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * qt + 4 * q4 + r;
+        if (row < LQ && key < LK) S[row * SS + key] = acc[r];
+      }
     }
     wave_lds_sync();
     // ---- ProbSparse: M per query from its sampled keys (sum over L_K), exact top-u by rank
@@ -362,9 +311,8 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
       wave_lds_sync();
     }
     const int nsel = sparse ? u : LQ;
-    // ---- softmax(scale · S) of the selected rows, P over S (zero beyond the row's last key).  Up to 32
-    //      rows: lanes l and l + 32 share row l & 31, each taking every other key, combined by the
-    //      32-lane swap; more rows: one lane per row.
+    // ---- softmax(scale · S) of the selected rows in place (keys beyond the row's last one: zero).  Up to 32
+    //      rows: lanes l and l + 32 share row l & 31, each taking every other key; more rows: one lane per row.
     if (nsel <= 32) {
       const int r = lane & 31, half = lane >> 5;
       const bool act = r < nsel;
@@ -374,10 +322,9 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
       float mx = -INFINITY;
 #pragma unroll 4
       for (int j = half; j < kmax; j += 2) mx = fmaxf(mx, row[j] * scale);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));   // ds_bpermute: the scan (tools/exec_scan.py) cannot follow
-                                                 // this function's spilled EXEC masks to clear a swap here
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));   // ds_bpermute (a convergent cross-lane read)
       float sum = 0.f;
-      const int kend = act ? LKp : 0;
+      const int kend = act ? LK : 0;
 #pragma unroll 4
       for (int j = half; j < kend; j += 2) {
         const float p = j < kmax ? expf(row[j] * scale - mx) : 0.f;
@@ -398,7 +345,7 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
         for (int j = 0; j < kmax; ++j) mx = fmaxf(mx, row[j] * scale);
         float sum = 0.f;
 #pragma unroll 8
-        for (int j = 0; j < LKp; ++j) {
+        for (int j = 0; j < LK; ++j) {
           const float p = j < kmax ? expf(row[j] * scale - mx) : 0.f;
           row[j] = p;
           sum += p;
@@ -436,8 +383,9 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
       const int e = 16 * et + r16;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       for (int k0 = 0; k0 < LKp; k0 += 4) {
-        const float a = S[qa * SS + k0 + q4];
-        const float b = e < E ? V[(k0 + q4) * ldv + hc + e] : 0.f;
+        const int k = k0 + q4;
+        const float a = k < LK ? S[qa * SS + k] : 0.f;
+        const float b = e < E ? V[k * ldv + hc + e] : 0.f;
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
       }
 #pragma unroll
@@ -449,14 +397,6 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
     wave_lds_sync();   // S / sel of this head read before the next head's scores overwrite them
   }
 }
-
-#ifdef LWF_PRE_ON
-#define LWF_PRE(name, g) const FPre name = fpre(blob, pw, g)
-#define LWF_PP(name) &name
-#else
-#define LWF_PRE(name, g)
-#define LWF_PP(name) nullptr
-#endif
 
 #ifdef LWF_STAMPS
 // diagnostic build: cycles of workgroup 0 per category (0 GEMM, 1 attention, 2 LayerNorm, 3 other), printed
@@ -470,7 +410,9 @@ __device__ LWF_OP_LINK void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, int 
 #define LWF_ST_END
 #endif
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) lw_fused(
+// NC: LayerNorm chunks of 16 features per lane row (d_model ≤ 16·NC)
+template <int NC>
+__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) lw_fused(
     const FPlan* __restrict__ p, const float* __restrict__ blob, const float* __restrict__ pw,
     const float* __restrict__ x_enc, const float* __restrict__ x_dec, float* __restrict__ out,
     const int32_t* __restrict__ idx) {
@@ -480,34 +422,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
   const int D = p->D, H = p->H, E = p->E, HE = p->HE, L0 = p->L0, Ld = p->Ld;
   const int ldD = p->ldD, ldT = p->ldT, ldH = p->ldH, ldF = p->ldF, ldKV = p->ldKV;
   // LDS regions (float offsets into lsm)
-  const int E0 = p->oE0, X = p->oX, T = p->oT, CTX = p->oCTX, ENC = p->oENC, XD = p->oXD;
-  const int scr = p->oSCR + w * p->scr_floats;
+  const int E1 = p->oE1, X = p->oX, T = p->oT, CTX = p->oCTX, ENC = p->oENC, XD = p->oXD;
+  const int AW = p->attn_waves;
+  const int scr = p->oSCR + (w < AW ? w : 0) * p->scr_floats;
   // zero LDS (padded rows and columns stay finite: they only ever meet zero weights or masked keys), then
   // stage this sequence's encoder input rows
-  for (int i = tid; i < p->lds_floats; i += 256) lsm[i] = 0.f;
+  for (int i = tid; i < p->lds_floats; i += NTH) lsm[i] = 0.f;
   __syncthreads();
   LWF_ST(3)
   {
     const int C = p->C, ldIN = p->ldIN;
     const float* xe = x_enc + (size_t)b * L0 * C;
-    for (int i = tid; i < L0 * C; i += 256) {
+    for (int i = tid; i < L0 * C; i += NTH) {
       const int t = i / C;
       lsm[T + t * ldIN + (i - t * C)] = xe[i];
     }
   }
   __syncthreads();
   LWF_ST(3)
-  // ---- DataEmbedding of the encoder input
-  fgemm<1>(blob, pw, p->emb_e, T, p->ldIN, p->C, L0, p->stack ? E0 : X, ldD, blob + p->pe_e, 0, 0);
+  // ---- DataEmbedding of the encoder input, straight into encoder 0's rows; a stack keeps the rows of the
+  //      later encoders' windows x[:, -L0/2:] (each later window is a suffix of it) in E1
+  fgemm<1>(blob, pw, p->emb_e, T, p->ldIN, p->C, L0, X, ldD, blob + p->pe_e, 0, 0);
   __syncthreads();
   LWF_ST(0)
+  const int e1rows = p->e1_rows;
+  if (e1rows > 0) {
+    for (int k = tid; k < e1rows * D; k += NTH) {
+      const int t = k / D, c = k - t * D;
+      lsm[E1 + t * ldD + c] = lsm[X + (L0 - e1rows + t) * ldD + c];
+    }
+    __syncthreads();
+    LWF_ST(3)
+  }
   // ---- encoders
   for (int i = 0; i < p->nenc; ++i) {
     int L = p->eL0[i];
-    if (p->stack) {   // x[:, -L:] of the embedded input
-      for (int k = tid; k < L * D; k += 256) {
+    if (i > 0) {   // x[:, -L:] of the embedded input
+      for (int k = tid; k < L * D; k += NTH) {
         const int t = k / D, c = k - t * D;
-        lsm[X + t * ldD + c] = lsm[E0 + (L0 - L + t) * ldD + c];
+        lsm[X + t * ldD + c] = lsm[E1 + (e1rows - L + t) * ldD + c];
       }
       __syncthreads();
       LWF_ST(3)
@@ -522,26 +475,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
         const int u = call >= 0 ? p->call_u[call] : L;
         const int sparse = p->prob && call >= 0 && u < L;
         fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
-              u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
+              u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
       }
-      LWF_PRE(po, ly->o);
       __syncthreads();
       LWF_ST(1)
-      fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(po));   // x + attention (encoder.py:44-49)
+      fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
       __syncthreads();
       LWF_ST(0)
-      fln(X, ldD, L, D, blob + ly->g1, blob + ly->b1, X, ldD);
-      LWF_PRE(pf1, ly->f1);
+      fln<NC>(X, ldD, L, D, blob + ly->g1, blob + ly->b1, X, ldD);
       __syncthreads();
       LWF_ST(2)
-      fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0, nullptr, 0, 0, LWF_PP(pf1));
-      LWF_PRE(pf2, ly->f2);
+      fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
       __syncthreads();
       LWF_ST(0)
-      fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(pf2));
+      fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
       __syncthreads();
       LWF_ST(0)
-      fln(X, ldD, L, D, blob + ly->g2, blob + ly->b2, X, ldD);
+      fln<NC>(X, ldD, L, D, blob + ly->g2, blob + ly->b2, X, ldD);
       __syncthreads();
       LWF_ST(2)
       if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
@@ -549,7 +499,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
         __syncthreads();
         LWF_ST(0)
         const int Lo = ly->Lo;
-        for (int k = tid; k < Lo * D; k += 256) {
+        for (int k = tid; k < Lo * D; k += NTH) {
           const int t = k / D, c = k - t * D;
           float v = lsm[T + (2 * t) * ldF + c];
           if (2 * t + 1 < L) v = fmaxf(v, lsm[T + (2 * t + 1) * ldF + c]);
@@ -562,7 +512,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
       }
     }
     // Encoder.norm → rows [eoff, eoff + L) of the concatenated stack output
-    fln(X, ldD, L, D, blob + p->ng[i], blob + p->nb[i], ENC + p->eoff[i] * ldD, ldD);
+    fln<NC>(X, ldD, L, D, blob + p->ng[i], blob + p->nb[i], ENC + p->eoff[i] * ldD, ldD);
     __syncthreads();
     LWF_ST(2)
   }
@@ -570,7 +520,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
   {
     const int Cd = p->Cd, ldIN = p->ldINd;
     const float* xd = x_dec + (size_t)b * Ld * Cd;
-    for (int i = tid; i < Ld * Cd; i += 256) {
+    for (int i = tid; i < Ld * Cd; i += NTH) {
       const int t = i / Cd;
       lsm[T + t * ldIN + (i - t * Cd)] = xd[i];
     }
@@ -592,44 +542,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
       const int u = call >= 0 ? p->call_u[call] : Ld;
       const int sparse = p->prob && call >= 0 && u < Ld;
       fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
-            call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr);
+            call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
     }
-    LWF_PRE(po, ly->o);
     __syncthreads();
     LWF_ST(1)
-    fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(po));   // norm1(x + self-attention)
+    fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
     __syncthreads();
     LWF_ST(0)
-    fln(XD, ldD, Ld, D, blob + ly->g1, blob + ly->b1, XD, ldD);
+    fln<NC>(XD, ldD, Ld, D, blob + ly->g1, blob + ly->b1, XD, ldD);
     __syncthreads();
     LWF_ST(2)
     fgemm<0>(blob, pw, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
     fgemm<0>(blob, pw, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
-    fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr);
-    LWF_PRE(pco, ly->co);
+    fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
     __syncthreads();
     LWF_ST(1)
-    fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(pco));   // norm2(x + cross-attention)
+    fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
     __syncthreads();
     LWF_ST(0)
-    fln(XD, ldD, Ld, D, blob + ly->g2, blob + ly->b2, XD, ldD);
-    LWF_PRE(pf1, ly->f1);
+    fln<NC>(XD, ldD, Ld, D, blob + ly->g2, blob + ly->b2, XD, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0, nullptr, 0, 0, LWF_PP(pf1));
-    LWF_PRE(pf2, ly->f2);
+    fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
     __syncthreads();
     LWF_ST(0)
-    fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0, LWF_PP(pf2));   // norm3(x + y)
+    fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
     __syncthreads();
     LWF_ST(0)
-    fln(XD, ldD, Ld, D, blob + ly->g3, blob + ly->b3, XD, ldD);
+    fln<NC>(XD, ldD, Ld, D, blob + ly->g3, blob + ly->b3, XD, ldD);
     __syncthreads();
     LWF_ST(2)
   }
-  fln(XD, ldD, Ld, D, blob + p->dng, blob + p->dnb, XD, ldD);
+  fln<NC>(XD, ldD, Ld, D, blob + p->dng, blob + p->dnb, XD, ldD);
   __syncthreads();
   LWF_ST(2)
   // projection of the last pred_len rows → out[b][pred][c_out]
@@ -639,15 +585,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) l
   LWF_ST_END
 }
 
-int prepare_fused() {
-  return cet::ensure_lds_attr(reinterpret_cast<const void*>(lw_fused)) ? 0 : -1;
+// the instance of a plan: four LayerNorm chunks per lane row up to d_model 64, sixteen up to 256
+static const void* kernel_of(int D) {
+  return D <= 64 ? reinterpret_cast<const void*>(lw_fused<4>) : reinterpret_cast<const void*>(lw_fused<16>);
 }
 
-int launch_fused(const FPlan* d_plan, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
+int prepare_fused(int D) {
+  return cet::ensure_lds_attr(kernel_of(D)) ? 0 : -1;
+}
+
+int launch_fused(const FPlan* d_plan, int D, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
                  const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st) {
   if (B <= 0) return 0;
-  if (prepare_fused()) return -1;
-  hipLaunchKernelGGL(lw_fused, dim3(B), dim3(256), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
+  if (prepare_fused(D)) return -1;
+  if (D <= 64)
+    hipLaunchKernelGGL(lw_fused<4>, dim3(B), dim3(NTH), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
+  else
+    hipLaunchKernelGGL(lw_fused<16>, dim3(B), dim3(NTH), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
