@@ -33,6 +33,15 @@ constexpr float NEG_INF = -__builtin_inff();
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// Thread index the compiler cannot hoist: loop-invariant per-lane addresses of once-per-call copies
+// (count tables, sampler state) would otherwise be computed at the encoder loop's entry and live, spilled,
+// across the whole kernel.
+__device__ __forceinline__ int tid_op() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  __builtin_assume(t >= 0 && t < 1024);
+  return t;
+}
 
 __device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);

@@ -129,7 +129,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + c.cnt_off);
         f32x4* dst = reinterpret_cast<f32x4*>(CNT);
 #ifndef CET_ABL_CNT
-        for (int i = threadIdx.x; i < bytes / 16; i += NTHREADS) dst[i] = src[i];
+        for (int i = tid_op(); i < bytes / 16; i += NTHREADS) dst[i] = src[i];
         __syncthreads();
 #else
         (void)bytes; (void)src; (void)dst;   // ablation (wrong results)

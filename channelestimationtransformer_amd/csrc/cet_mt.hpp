@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t 
 template <int NT>
 __device__ __forceinline__ void mt_twist(uint32_t* st) {
   static_assert(NT >= 227, "one word per thread per third");
-  const int t = threadIdx.x;
+  const int t = tid_op();
   __syncthreads();   // every reader of the previous block is done
   uint32_t n0 = 0, n1 = 0, n2 = 0;
   if (t < 227) {
@@ -70,7 +70,7 @@ template <int NT>
 __device__ __forceinline__ void mt_replay(MTState& g, int LQ, int U, int LK, uint32_t* tab, int stride) {
   if (tab) {
     const int words = ((LQ + 15) & ~15) * stride / 4;
-    for (int i = threadIdx.x; i < words; i += NT) tab[i] = 0u;
+    for (int i = tid_op(); i < words; i += NT) tab[i] = 0u;
     __syncthreads();
   }
   const int n = LQ * U;
@@ -83,7 +83,7 @@ __device__ __forceinline__ void mt_replay(MTState& g, int LQ, int U, int LK, uin
     }
     const int take = min(MT_N - g.idx, n - done);
     if (tab) {
-      for (int t = threadIdx.x; t < take; t += NT) {
+      for (int t = tid_op(); t < take; t += NT) {
         const uint32_t key = mt_temper(g.st[g.idx + t]) % (uint32_t)LK;
         const int q = (int)(((float)(done + t) + 0.5f) * invU);   // exact: p < 96·96, U ≤ 96
         atomicAdd(&tab[(q * stride + cnt_word_off((int)key)) >> 2], 1u << ((key & 3u) * 8u));   // counts ≤ U < 256
@@ -97,14 +97,14 @@ __device__ __forceinline__ void mt_replay(MTState& g, int LQ, int U, int LK, uin
 
 template <int NT>
 __device__ __forceinline__ void mt_load(MTState& g, const uint32_t* __restrict__ src) {
-  for (int i = threadIdx.x; i < MT_N; i += NT) g.st[i] = src[i];
+  for (int i = tid_op(); i < MT_N; i += NT) g.st[i] = src[i];
   g.idx = (int)src[MT_N];
   __syncthreads();
 }
 
 template <int NT>
 __device__ __forceinline__ void mt_store(const MTState& g, uint32_t* __restrict__ dst) {
-  for (int i = threadIdx.x; i < MT_N; i += NT) dst[i] = g.st[i];
+  for (int i = tid_op(); i < MT_N; i += NT) dst[i] = g.st[i];
   if (threadIdx.x == 0) dst[MT_N] = (uint32_t)g.idx;
 }
 

@@ -30,7 +30,7 @@ __device__ __forceinline__ void replay_all_calls(const InformerPlan& pl, const u
       typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
       const u32x4* src = reinterpret_cast<const u32x4*>(tab_lds);
       u32x4* dst = reinterpret_cast<u32x4*>(tab_out + ac.cnt_off);
-      for (int i = threadIdx.x; i < n16; i += NT) dst[i] = src[i];
+      for (int i = tid_op(); i < n16; i += NT) dst[i] = src[i];
       __syncthreads();   // the next call zeroes the LDS table
     }
   }
@@ -52,7 +52,7 @@ __device__ __forceinline__ void replay_all_fast(const InformerPlan& pl, const ui
   uint32_t* words = st + MT_WORDS;
   uint32_t* tabs = words + ((pl.draws + 3) & ~3);
   const int tab16 = (int)pl.cnt_bytes / 16;
-  for (int i = threadIdx.x; i < tab16; i += NT) reinterpret_cast<u32x4*>(tabs)[i] = u32x4{0u, 0u, 0u, 0u};
+  for (int i = tid_op(); i < tab16; i += NT) reinterpret_cast<u32x4*>(tabs)[i] = u32x4{0u, 0u, 0u, 0u};
   MTState g{st, MT_N};
   mt_load<NT>(g, mt_in);
   const int total = pl.draws;
@@ -63,7 +63,7 @@ __device__ __forceinline__ void replay_all_fast(const InformerPlan& pl, const ui
       g.idx = 0;
     }
     const int take = min(MT_N - g.idx, total - have);
-    for (int t = threadIdx.x; t < take; t += NT) words[have + t] = mt_temper(g.st[g.idx + t]);
+    for (int t = tid_op(); t < take; t += NT) words[have + t] = mt_temper(g.st[g.idx + t]);
     have += take;
     g.idx += take;
   }
@@ -75,7 +75,7 @@ __device__ __forceinline__ void replay_all_fast(const InformerPlan& pl, const ui
     if (ac.u < ac.LQ) {
       const float invU = 1.0f / (float)ac.U;
       uint32_t* tab = tabs + ac.cnt_off / 4;
-      for (int d = threadIdx.x; d < n; d += NT) {
+      for (int d = tid_op(); d < n; d += NT) {
         const uint32_t key = words[base + d] % (uint32_t)ac.LK;
         const int q = (int)(((float)d + 0.5f) * invU);   // exact: d < 96·96, U ≤ 96
         atomicAdd(&tab[(q * ac.cnt_stride + cnt_word_off((int)key)) >> 2], 1u << ((key & 3u) * 8u));
@@ -84,7 +84,7 @@ __device__ __forceinline__ void replay_all_fast(const InformerPlan& pl, const ui
     base += n;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < tab16; i += NT)
+  for (int i = tid_op(); i < tab16; i += NT)
     reinterpret_cast<u32x4*>(tab_out)[i] = reinterpret_cast<const u32x4*>(tabs)[i];
   mt_store<NT>(g, mt_out);
 }

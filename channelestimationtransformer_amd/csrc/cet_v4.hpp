@@ -796,7 +796,7 @@ template <int N>
 using IC = std::integral_constant<int, N>;
 
 __device__ __forceinline__ void stage(const float* __restrict__ src, float* dst, int L, int C, int CS) {
-  for (int i = threadIdx.x; i < L * C; i += NTHREADS) {
+  for (int i = tid_op(); i < L * C; i += NTHREADS) {
     const int t = i / C, c = i - t * C;
     dst[t * CS + c] = src[i];
   }
