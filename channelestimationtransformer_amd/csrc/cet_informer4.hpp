@@ -162,11 +162,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     for (int mt = 0; mt < MT; ++mt) X.v[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
       const GemmDesc d = PL.emb_enc;
-      gemm_res<PP, 2, MT>(M, d, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, off}, [&](int mt, int n0, f32x4 y) {
+      auto emb_epi = [&](int mt, int n0, f32x4 y) {
         const int m = mt * 16 + (lane_op() & 15);
         const int prow = m + off < LMAX ? m + off : LMAX - 1;
         X.v[mt] = y + pload4(M, PL.pe_enc, prow * DMODEL + n0);
-      });
+      };
+      gemm_res<PP, 2, MT>(M, d, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, off}, emb_epi);
     }
     if (stamps && e == 0 && threadIdx.x == 0) stamps[125] = __builtin_amdgcn_s_memtime();
     __syncthreads();                       // IN (aliases CTX) fully read

@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   LWF_ST(0)
   const int e1rows = p->e1_rows;
   if (e1rows > 0) {
-    for (int k = tid; k < e1rows * D; k += NTH) {
+    for (int k = tid_op(); k < e1rows * D; k += NTH) {
       const int t = k / D, c = k - t * D;
       lsm[E1 + t * ldD + c] = lsm[X + (L0 - e1rows + t) * ldD + c];
     }
@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   for (int i = 0; i < p->nenc; ++i) {
     int L = p->eL0[i];
     if (i > 0) {   // x[:, -L:] of the embedded input
-      for (int k = tid; k < L * D; k += NTH) {
+      for (int k = tid_op(); k < L * D; k += NTH) {
         const int t = k / D, c = k - t * D;
         lsm[X + t * ldD + c] = lsm[E1 + (e1rows - L + t) * ldD + c];
       }
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
         __syncthreads();
         LWF_ST(0)
         const int Lo = ly->Lo;
-        for (int k = tid; k < Lo * D; k += NTH) {
+        for (int k = tid_op(); k < Lo * D; k += NTH) {
           const int t = k / D, c = k - t * D;
           float v = lsm[T + (2 * t) * ldF + c];
           if (2 * t + 1 < L) v = fmaxf(v, lsm[T + (2 * t + 1) * ldF + c]);
@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   {
     const int Cd = p->Cd, ldIN = p->ldINd;
     const float* xd = x_dec + (size_t)b * Ld * Cd;
-    for (int i = tid; i < Ld * Cd; i += NTH) {
+    for (int i = tid_op(); i < Ld * Cd; i += NTH) {
       const int t = i / Cd;
       lsm[T + t * ldIN + (i - t * Cd)] = xd[i];
     }

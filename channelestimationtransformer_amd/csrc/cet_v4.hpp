@@ -616,16 +616,25 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     return f32x2{mean, inv};
   };
 #ifndef CET_LN_TWO_BARRIER
-  if constexpr (N == 1) {
-    // one m-tile (the decoder's 15 rows): every wave combines its own rows' partials — no second
-    // barrier; the caller's barrier after the LN orders these reads before the partials are rewritten
-    if (nmt > 0) {
-      const f32x2 st = row_stats(c);
-      const f32x4 y = (X.v[0] - st[0]) * st[1] * g0 + b0;
-      if (INPLACE) X.v[0] = y;
-      if (c < rows) {
-        out.st4(c, nb, y);
-        if (out2) out2->st4(c, nb, y);
+#ifndef CET_LN_ONE_MAX
+#define CET_LN_ONE_MAX 1
+#endif
+  if constexpr (N <= CET_LN_ONE_MAX) {
+    // few m-tiles (the decoder's 15 rows): every wave combines its own rows' partials — no second
+    // barrier; the caller's barrier after the LN orders these reads before the partials are rewritten.
+    // For the encoder's 3-6 tiles the redundant combining costs more than the barrier it saves
+    // (-DCET_LN_ONE_MAX=3 ±0, =6 +1.2 us; profiles/r04/ab9/ab.log)
+#pragma unroll
+    for (int mt = 0; mt < N; ++mt) {
+      if (mt < nmt) {
+        const int m = mt * 16 + c;
+        const f32x2 st = row_stats(m);
+        const f32x4 y = (X.v[mt] - st[0]) * st[1] * g0 + b0;
+        if (INPLACE) X.v[mt] = y;
+        if (m < rows) {
+          out.st4(m, nb, y);
+          if (out2) out2->st4(m, nb, y);
+        }
       }
     }
     return;
