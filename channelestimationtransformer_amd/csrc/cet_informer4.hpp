@@ -31,9 +31,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   const int my_e = SPLIT ? (int)blockIdx.x - b * nsplit : -1;   // the one encoder of this workgroup
   if (b >= a.B) return;
   const int w = wave_id();
-#ifndef CET_NO_SETPRIO
+#ifdef CET_SETPRIO
   // static priority for the younger half of the workgroup, the SIMD arbitration loser
-  // (MI355X_MICROARCH "Two waves per SIMD" item 4): −0.7 µs at C2 (profiles/r02/ab_erf_setprio.log)
+  // (MI355X_MICROARCH "Two waves per SIMD" item 4): −0.7 µs at C2 with one batch in flight in round 2
+  // (profiles/r02/ab_erf_setprio.log); with two batches in flight and round 4's kernel it costs 2 % of the
+  // throughput at an equal kernel-alone time (profiles/r04/ab10/ab.log), so it is off by default
   if (w >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
 
