@@ -114,7 +114,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   };
   // the ProbSparse draws of one attention call: u, the multiplicity table (replayed in-kernel or staged)
   auto call_setup = [&](HeadIO<P>& io, int call) __attribute__((always_inline)) {
+#ifndef CET_STAMP_DEC_CALL
     io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
+#else   // diagnostic: sub-phases of the first encoder call and the first decoder self-attention call
+    io.st = (stamps && (call == 0 || call == PL.n_calls - 3)) ? stamps + 100 + 8 * (call != 0) : nullptr;
+#endif
     if (call >= 0) {
       const AttnCall& c = PL.calls[call];
       io.u = c.u;

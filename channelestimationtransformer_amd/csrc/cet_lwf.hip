@@ -115,10 +115,12 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
 #pragma unroll
     for (int i = 0; i < KW; ++i) wa[i] = wp[(size_t)(i < KQ ? i : 0) * 64];
     for (int kc = 0; kc < KQ; kc += KW) {
+      if (kc + KW < KQ) {   // uniform: the last window requests nothing more
 #pragma unroll
-      for (int i = 0; i < KW; ++i) {
-        const int kq = kc + KW + i;
-        wb[i] = wp[(size_t)(kq < KQ ? kq : 0) * 64];
+        for (int i = 0; i < KW; ++i) {
+          const int kq = kc + KW + i;
+          wb[i] = wp[(size_t)(kq < KQ ? kq : 0) * 64];
+        }
       }
 #pragma unroll
       for (int i = 0; i < KW; ++i) {
@@ -141,8 +143,10 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
             for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][m], wa[i][j], acc[m], 0, 0, 0);
         }
       }
+      if (kc + KW < KQ) {
 #pragma unroll
-      for (int i = 0; i < KW; ++i) wa[i] = wb[i];
+        for (int i = 0; i < KW; ++i) wa[i] = wb[i];
+      }
     }
     if (n >= N) continue;
 #pragma unroll
