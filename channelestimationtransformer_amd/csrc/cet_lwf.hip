@@ -189,20 +189,31 @@ __device__ __forceinline__ void fgemm(const float* __restrict__ blob, const floa
 
 // LayerNorm of L rows of width D ≤ 16·NC (eps 1e-5, biased variance; encoder.py:49-56): four rows per wave at
 // a time, 16 lanes per row; Y may alias X.
+// The lane's γ / β columns, requested ahead (before the barrier that precedes the LayerNorm).
 template <int NC>
-__device__ __forceinline__ void fln(int X, int ldx, int L, int D, const float* __restrict__ g,
-                                    const float* __restrict__ bb, int Y, int ldy) {
+struct LnPre {
+  float g[NC], b[NC];
+};
+template <int NC>
+__device__ __forceinline__ LnPre<NC> lnpre(const float* __restrict__ g, const float* __restrict__ bb, int D) {
+  LnPre<NC> p;
+  const int r16 = threadIdx.x & 15;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = r16 + 16 * i;
+    p.g[i] = c < D ? g[c] : 0.f;
+    p.b[i] = c < D ? bb[c] : 0.f;
+  }
+  return p;
+}
+template <int NC>
+__device__ __forceinline__ void fln(int X, int ldx, int L, int D, const LnPre<NC>& pp, int Y, int ldy) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   X = uni(X); ldx = uni(ldx); L = uni(L); D = uni(D); Y = uni(Y); ldy = uni(ldy);
   const int r16 = lane & 15, sub = lane >> 4;
   const float invD = 1.0f / (float)D;
-  float gv[NC], bv[NC];
-#pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const int c = r16 + 16 * i;
-    gv[i] = c < D ? g[c] : 0.f;
-    bv[i] = c < D ? bb[c] : 0.f;
-  }
+  const float* gv = pp.g;
+  const float* bv = pp.b;
   for (int t0 = 4 * w; t0 < L; t0 += 4 * NW) {
     const int t = t0 + sub;
     const bool on = t < L;
@@ -484,18 +495,20 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       __syncthreads();
       LWF_ST(1)
       fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
+      const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
       __syncthreads();
       LWF_ST(0)
-      fln<NC>(X, ldD, L, D, blob + ly->g1, blob + ly->b1, X, ldD);
+      fln<NC>(X, ldD, L, D, n1, X, ldD);
       __syncthreads();
       LWF_ST(2)
       fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
       __syncthreads();
       LWF_ST(0)
       fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
+      const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
       __syncthreads();
       LWF_ST(0)
-      fln<NC>(X, ldD, L, D, blob + ly->g2, blob + ly->b2, X, ldD);
+      fln<NC>(X, ldD, L, D, n2, X, ldD);
       __syncthreads();
       LWF_ST(2)
       if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
@@ -516,7 +529,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       }
     }
     // Encoder.norm → rows [eoff, eoff + L) of the concatenated stack output
-    fln<NC>(X, ldD, L, D, blob + p->ng[i], blob + p->nb[i], ENC + p->eoff[i] * ldD, ldD);
+    fln<NC>(X, ldD, L, D, lnpre<NC>(blob + p->ng[i], blob + p->nb[i], D), ENC + p->eoff[i] * ldD, ldD);
     __syncthreads();
     LWF_ST(2)
   }
@@ -551,9 +564,10 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     __syncthreads();
     LWF_ST(1)
     fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
+    const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
     __syncthreads();
     LWF_ST(0)
-    fln<NC>(XD, ldD, Ld, D, blob + ly->g1, blob + ly->b1, XD, ldD);
+    fln<NC>(XD, ldD, Ld, D, n1, XD, ldD);
     __syncthreads();
     LWF_ST(2)
     fgemm<0>(blob, pw, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
@@ -564,22 +578,24 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     __syncthreads();
     LWF_ST(1)
     fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
+    const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
     __syncthreads();
     LWF_ST(0)
-    fln<NC>(XD, ldD, Ld, D, blob + ly->g2, blob + ly->b2, XD, ldD);
+    fln<NC>(XD, ldD, Ld, D, n2, XD, ldD);
     __syncthreads();
     LWF_ST(2)
     fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
     __syncthreads();
     LWF_ST(0)
     fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
+    const LnPre<NC> n3 = lnpre<NC>(blob + ly->g3, blob + ly->b3, D);
     __syncthreads();
     LWF_ST(0)
-    fln<NC>(XD, ldD, Ld, D, blob + ly->g3, blob + ly->b3, XD, ldD);
+    fln<NC>(XD, ldD, Ld, D, n3, XD, ldD);
     __syncthreads();
     LWF_ST(2)
   }
-  fln<NC>(XD, ldD, Ld, D, blob + p->dng, blob + p->dnb, XD, ldD);
+  fln<NC>(XD, ldD, Ld, D, lnpre<NC>(blob + p->dng, blob + p->dnb, D), XD, ldD);
   __syncthreads();
   LWF_ST(2)
   // projection of the last pred_len rows → out[b][pred][c_out]
