@@ -1,8 +1,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 L=channelestimationtransformer_amd
-O=gpurun_out/lw6; mkdir -p $O
-CET_LIB=$(pwd)/$L/libcet_lwgp.so timeout -k 10 600 python -u -m pytest tests/test_gpu_layerwise.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests_lwgp.log 2>&1 || { tail -30 $O/tests_lwgp.log; exit 1; }
-echo "lwgp $(tail -1 $O/tests_lwgp.log)"
-for i in 1 2; do for v in _lwbase _lwgp; do echo "libcet$v: $(CET_LIB=$(pwd)/$L/libcet$v.so timeout -k 10 120 python tools/d64_time.py 512 200)"; done; done | tee $O/d64.log
+O=gpurun_out/lw7; mkdir -p $O
+CET_LIB=$(pwd)/$L/libcet_lwsm.so timeout -k 10 600 python -u -m pytest tests/test_gpu_layerwise.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests_lwsm.log 2>&1 || { tail -30 $O/tests_lwsm.log; exit 1; }
+echo "lwsm $(tail -1 $O/tests_lwsm.log)"
+for i in 1 2; do for v in _lwbase _lwsm; do echo "libcet$v: $(CET_LIB=$(pwd)/$L/libcet$v.so timeout -k 10 120 python tools/d64_time.py 512 200)"; done; done | tee $O/d64.log
 echo done
