@@ -1,4 +1,5 @@
-"""Build guard (CPU): no cross-lane swap of the shipped gfx950 code runs under a narrowed EXEC.
+"""Build guards (CPU) on the shipped gfx950 code: no cross-lane swap runs under a narrowed EXEC, and the
+production fused kernels keep their scratch (VGPR-spill) footprint small.
 
 The v4 kernels and the fused layer-wise form reduce across lanes with v_permlane16_swap /
 v_permlane32_swap; a butterfly is only right when every lane takes part, and the compiler once sank
@@ -63,3 +64,26 @@ def test_scan_flags_swaps_in_divergent_regions(lines, flag):
 
     (name, body), = list(exec_scan.functions(_fn(lines)))
     assert bool(exec_scan.scan_function(body)) == flag
+
+
+# The production C2 instance's scratch per lane (tools/kernel_resources.py): 52 B since the once-per-call copy
+# loops stopped hoisting their per-lane addresses (136 B before, which wrote 26 MiB of spill
+# scratch per launch).  A regression past this budget brings the spill traffic back.
+SCRATCH_BUDGET = {
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0E": 64,    # C2 production (bf16)
+    "_ZN3cet2v422transformer_forward_v4ILi64ELb0E": 16,         # C3 production
+    "_ZN3cet2lw8lw_fusedILi4E": 32,                             # fused layer-wise form, d_model <= 64
+}
+
+
+def test_production_kernels_scratch_budget():
+    import kernel_resources
+
+    if not os.path.exists(LIB):
+        pytest.skip("libcet.so not built")
+    res = kernel_resources.resources(LIB)
+    for prefix, budget in SCRATCH_BUDGET.items():
+        hits = {n: v for n, v in res.items() if n.startswith(prefix)}
+        assert hits, f"kernel {prefix}… not found in libcet.so"
+        for name, v in hits.items():
+            assert v.get("private_segment_fixed_size", 0) <= budget, (name, v)
