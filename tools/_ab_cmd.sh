@@ -1,10 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-L=channelestimationtransformer_amd
-O=gpurun_out/ab16; mkdir -p $O
-for v in lnf; do
-  CET_LIB=$(pwd)/$L/libcet_$v.so timeout -k 10 600 python -u -m pytest tests/test_gpu_informer.py tests/test_gpu_inflight.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests_$v.log 2>&1 || { tail -30 $O/tests_$v.log; exit 1; }
-  echo "$v $(tail -1 $O/tests_$v.log)"
-done
-bash tools/ab_bench.sh $L/libcet.so $L/libcet_lnf.so | tee $O/ab.log || exit 1
+bash tools/session.sh r04h tests smoke configs || exit 1
+timeout -k 10 300 python bench.py > gpurun_out/r04h/bench.json 2> gpurun_out/r04h/bench.err || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r04h/bench_steps20.json 2> gpurun_out/r04h/bench_steps20.err || exit 1
+cut -c1-250 gpurun_out/r04h/bench.json gpurun_out/r04h/bench_steps20.json
 echo done
