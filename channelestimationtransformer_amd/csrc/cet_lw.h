@@ -114,9 +114,10 @@ struct FPlan {
   FEnc enc[F_MAX_ENC][F_MAX_EL];
   FDec dec[F_MAX_DEC];
 };
-int launch_fused(const FPlan* d_plan, int D, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
+bool plan_is_d64(const FPlan& p);   // the plan equals the compile-time d_model-64 layout (cet_lwf.hip D64Plan)
+int launch_fused(const FPlan* d_plan, int D, bool fix, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
                  const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st);
-int prepare_fused(int D);
+int prepare_fused(int D, bool fix);
 
 // ------------------------------------------------------------------ host model (cet_lw_host.cpp)
 // Weights as fp32 [N][K] matrices in one device blob (float offsets below); ProbSparse draws of a
@@ -172,6 +173,7 @@ struct Model {
   FPlan fplan{};
   bool fused_ok = false, use_fused = true, last_fused = false;
   size_t fused_lds = 0;
+  bool fused_fix = false;   // the plan is the compile-time d_model-64 layout (launch_fused's FIX instance)
   std::vector<float> pblob;
   FPlan* d_fplan = nullptr;
   float* d_pblob = nullptr;

@@ -163,7 +163,10 @@ int Model::build_fused() {
   if (hipMalloc((void**)&d_pblob, pblob.size() * sizeof(float)) != hipSuccess) return -1;
   if (hipMemcpy(d_pblob, pblob.data(), pblob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (hipMemcpy(d_fplan, &p, sizeof(FPlan), hipMemcpyHostToDevice) != hipSuccess) return -1;
-  if (prepare_fused(D)) return -1;
+  const char* fenv = std::getenv("CET_LW_FUSED_FIX");
+  fused_fix = plan_is_d64(p) && !(fenv && std::strcmp(fenv, "0") == 0);
+  if (why) fprintf(stderr, "lw fused: compile-time d64 layout %s\n", fused_fix ? "yes" : "no");
+  if (prepare_fused(D, fused_fix)) return -1;
   fused_ok = true;
   return 0;
 }
@@ -217,7 +220,7 @@ int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, fl
                    hipStream_t st) {
   // the fused form: one launch, no workspace, no staging copies
   last_fused = fused_ok && use_fused && !(attns && out_attn);
-  if (last_fused) return launch_fused(d_fplan, D, fused_lds, d_blob, d_pblob, x_enc, x_dec, out, idx_dev, B, st);
+  if (last_fused) return launch_fused(d_fplan, D, fused_fix, fused_lds, d_blob, d_pblob, x_enc, x_dec, out, idx_dev, B, st);
   if (ensure_ws(B)) return -1;
   if (attns && out_attn) return enqueue(x_enc, x_dec, B, out, attns, idx_dev, st);
   const Key key{x_enc, x_dec, out, idx_dev, B};
