@@ -74,14 +74,14 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in HBM instead of Y.  MT is compile-time, so the K loop is
 // straight-line code (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A
 // reads of k ≥ K land in the padded, finite part of the LDS image and meet zero weights.
-template <int AMODE, int MT>
+template <int AMODE, int MT, int NF = 0, int KF = 0>
 __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
                                         int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
                                         int act, int res, float* __restrict__ gout, int t0, int ldo, int m0, int n0,
                                         int nstep) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, q4 = lane >> 4;
-  const int N = uni(g.N), K = uni(g.K);
+  const int N = NF ? NF : uni(g.N), K = KF ? KF : uni(g.K);   // NF / KF: the plan's N / K at compile time
   const int NT = (N + 15) >> 4, KQ = (K + 15) >> 4;
   const bool has_b = uni(g.b) != (int)FNONE, has_s = uni(g.s) != (int)FNONE;
   // the lane's A rows (AMODE 0) / its three circular source rows per m-tile (AMODE 1)
@@ -171,19 +171,19 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
 
 // The GEMM's task split over the eight waves (≤ 48 rows: the plan's validated range, cet_lw_host.cpp
 // build_fused): two m-tiles are split between the wave halves, one or three stay whole per wave.
-template <int AMODE>
+template <int AMODE, int NF = 0, int KF = 0>
 __device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g, int A,
                                       int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe, int act,
                                       int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
   const int w = uni(threadIdx.x >> 6);
   A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
   switch ((L + 15) >> 4) {
-    case 1: fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    case 1: fgemm_t<AMODE, 1, NF, KF>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
     case 2:
-      fgemm_t<AMODE, 1>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, w / (NW / 2), w % (NW / 2),
+      fgemm_t<AMODE, 1, NF, KF>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, w / (NW / 2), w % (NW / 2),
                         NW / 2);
       break;
-    default: fgemm_t<AMODE, 3>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    default: fgemm_t<AMODE, 3, NF, KF>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
   }
 }
 
@@ -431,7 +431,8 @@ __device__ __forceinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, 
 // fold into immediates instead of occupying scalar registers across the forward); the host launches that
 // instance only when the plan's fields equal them (plan_is_d64).
 struct D64Plan {
-  static constexpr int D = 64, H = 8, E = 8, HE = 64, L0 = 25, Ld = 15, C = 16, Cd = 16, S = 7, nenc = 2, ndec = 3;
+  static constexpr int D = 64, H = 8, E = 8, HE = 64, dff = 64, L0 = 25, Ld = 15, C = 16, Cd = 16, S = 7, nenc = 2,
+                       ndec = 3;
   static constexpr int ldD = 66, ldT = 194, ldH = 66, ldF = 66, ldKV = 130, ldIN = 17, ldINd = 17;
   static constexpr int oE1 = 0, e1_rows = 12, oX = 792, oT = 2904, oCTX = 9112, oENC = 11224, oXD = 12280;
   static constexpr int oSCR = 13336, scr_floats = 748, attn_waves = 8, lds_floats = 19320, pred = 5, c_out = 16;
@@ -472,7 +473,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   LWF_ST(3)
   // ---- DataEmbedding of the encoder input, straight into encoder 0's rows; a stack keeps the rows of the
   //      later encoders' windows x[:, -L0/2:] (each later window is a suffix of it) in E1
-  fgemm<1>(blob, pw, p->emb_e, T, PV(ldIN), PV(C), L0, X, ldD, blob + p->pe_e, 0, 0);
+  fgemm<1, FIX ? 64 : 0, FIX ? 48 : 0>(blob, pw, p->emb_e, T, PV(ldIN), PV(C), L0, X, ldD, blob + p->pe_e, 0, 0);
   __syncthreads();
   LWF_ST(0)
   const int e1rows = PV(e1_rows);
@@ -499,7 +500,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     #pragma unroll 1
     for (int l = 0; l < PA(nl, i); ++l) {
       const FEnc* ly = &p->enc[i][l];
-      fgemm<0>(blob, pw, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
+      fgemm<0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
       __syncthreads();
       LWF_ST(0)
       {
@@ -511,17 +512,17 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       }
       __syncthreads();
       LWF_ST(1)
-      fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
+      fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
       const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
       __syncthreads();
       LWF_ST(0)
       fln<NC>(X, ldD, L, D, n1, X, ldD);
       __syncthreads();
       LWF_ST(2)
-      fgemm<0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
+      fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
       __syncthreads();
       LWF_ST(0)
-      fgemm<0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
+      fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
       const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
       __syncthreads();
       LWF_ST(0)
@@ -529,7 +530,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       __syncthreads();
       LWF_ST(2)
       if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
-        fgemm<1>(blob, pw, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
+        fgemm<1, FIX ? 64 : 0, FIX ? 192 : 0>(blob, pw, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
         __syncthreads();
         LWF_ST(0)
         const int Lo = ly->Lo;
@@ -561,7 +562,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   }
   __syncthreads();
   LWF_ST(3)
-  fgemm<1>(blob, pw, p->emb_d, T, PV(ldINd), PV(Cd), Ld, XD, ldD, blob + p->pe_d, 0, 0);
+  fgemm<1, FIX ? 64 : 0, FIX ? 48 : 0>(blob, pw, p->emb_d, T, PV(ldINd), PV(Cd), Ld, XD, ldD, blob + p->pe_d, 0, 0);
   __syncthreads();
   LWF_ST(0)
   const int S = PV(S);
@@ -569,7 +570,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   #pragma unroll 1
   for (int l = 0; l < PV(ndec); ++l) {
     const FDec* ly = &p->dec[l];
-    fgemm<0>(blob, pw, ly->qkv, XD, ldD, 0, Ld, T, ldT, nullptr, 0, 0);
+    fgemm<0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, ly->qkv, XD, ldD, 0, Ld, T, ldT, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
     {
@@ -581,31 +582,31 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     }
     __syncthreads();
     LWF_ST(1)
-    fgemm<0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
     const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
     __syncthreads();
     LWF_ST(0)
     fln<NC>(XD, ldD, Ld, D, n1, XD, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0>(blob, pw, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
-    fgemm<0>(blob, pw, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
+    fgemm<0, FIX ? 128 : 0, FIX ? 64 : 0>(blob, pw, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
     fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
     __syncthreads();
     LWF_ST(1)
-    fgemm<0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
     const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
     __syncthreads();
     LWF_ST(0)
     fln<NC>(XD, ldD, Ld, D, n2, XD, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
     __syncthreads();
     LWF_ST(0)
-    fgemm<0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
     const LnPre<NC> n3 = lnpre<NC>(blob + ly->g3, blob + ly->b3, D);
     __syncthreads();
     LWF_ST(0)
@@ -617,7 +618,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   __syncthreads();
   LWF_ST(2)
   // projection of the last pred_len rows → out[b][pred][c_out]
-  fgemm<0>(blob, pw, p->proj, XD, ldD, 0, Ld, 0, 0, nullptr, 0, 0, out + (size_t)b * PV(pred) * PV(c_out), Ld - PV(pred),
+  fgemm<0, FIX ? 16 : 0, FIX ? 64 : 0>(blob, pw, p->proj, XD, ldD, 0, Ld, 0, 0, nullptr, 0, 0, out + (size_t)b * PV(pred) * PV(c_out), Ld - PV(pred),
            PV(c_out));
   LWF_ST(0)
   LWF_ST_END
@@ -633,7 +634,7 @@ static const void* kernel_of(int D, bool fix) {
 
 bool plan_is_d64(const FPlan& p) {
   using Q = D64Plan;
-  bool ok = p.D == Q::D && p.H == Q::H && p.E == Q::E && p.HE == Q::HE && p.L0 == Q::L0 && p.Ld == Q::Ld &&
+  bool ok = p.D == Q::D && p.H == Q::H && p.E == Q::E && p.HE == Q::HE && p.dff == Q::dff && p.L0 == Q::L0 && p.Ld == Q::Ld &&
             p.C == Q::C && p.Cd == Q::Cd && p.S == Q::S && p.nenc == Q::nenc && p.ndec == Q::ndec &&
             p.ldD == Q::ldD && p.ldT == Q::ldT && p.ldH == Q::ldH && p.ldF == Q::ldF && p.ldKV == Q::ldKV &&
             p.ldIN == Q::ldIN && p.ldINd == Q::ldINd && p.oE1 == Q::oE1 && p.e1_rows == Q::e1_rows && p.oX == Q::oX &&
