@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "cet_device.hpp"
 #include "cet_lw.h"
 
@@ -37,6 +39,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int NW = 8;              // waves per workgroup
 constexpr int NTH = NW * 64;       // threads per workgroup
 constexpr int KW = 4;              // k-quads (16 k each) of weights per register window
+template <int N>
+using ICn = std::integral_constant<int, N>;
 
 __device__ __forceinline__ float fgelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
@@ -485,71 +489,96 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     __syncthreads();
     LWF_ST(3)
   }
-  // ---- encoders
-  #pragma unroll 1
-  for (int i = 0; i < PV(nenc); ++i) {
-    int L = PA(eL0, i);
-    if (i > 0) {   // x[:, -L:] of the embedded input
-      for (int k = tid_op(); k < L * D; k += NTH) {
+  // ---- encoders.  One encoder layer of rows L (a compile-time constant in the checkpoint instance, so its
+  //      GEMM tile counts and attention bounds fold); returns the rows after its distil conv.
+  auto enc_layer = [&](auto Lc, int i, int l) __attribute__((always_inline)) {
+    const int L = Lc;
+    int Lout = L;
+    const FEnc* ly = &p->enc[i][l];
+    fgemm<0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
+    __syncthreads();
+    LWF_ST(0)
+    {
+      const int call = ly->call;
+      const int u = call >= 0 ? p->call_u[call] : L;
+      const int sparse = p->prob && call >= 0 && u < L;
+      fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
+            u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
+    }
+    __syncthreads();
+    LWF_ST(1)
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
+    const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
+    __syncthreads();
+    LWF_ST(0)
+    fln<NC>(X, ldD, L, D, n1, X, ldD);
+    __syncthreads();
+    LWF_ST(2)
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
+    __syncthreads();
+    LWF_ST(0)
+    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
+    const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
+    __syncthreads();
+    LWF_ST(0)
+    fln<NC>(X, ldD, L, D, n2, X, ldD);
+    __syncthreads();
+    LWF_ST(2)
+    if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
+      fgemm<1, FIX ? 64 : 0, FIX ? 192 : 0>(blob, pw, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
+      __syncthreads();
+      LWF_ST(0)
+      const int Lo = ly->Lo;
+      for (int k = tid_op(); k < Lo * D; k += NTH) {
         const int t = k / D, c = k - t * D;
-        lsm[X + t * ldD + c] = lsm[E1 + (e1rows - L + t) * ldD + c];
+        float v = lsm[T + (2 * t) * ldF + c];
+        if (2 * t + 1 < L) v = fmaxf(v, lsm[T + (2 * t + 1) * ldF + c]);
+        if (2 * t - 1 >= 0) v = fmaxf(v, lsm[T + (2 * t - 1) * ldF + c]);
+        lsm[X + t * ldD + c] = v;
       }
       __syncthreads();
       LWF_ST(3)
+      Lout = Lo;
     }
-    #pragma unroll 1
-    for (int l = 0; l < PA(nl, i); ++l) {
-      const FEnc* ly = &p->enc[i][l];
-      fgemm<0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
-      __syncthreads();
-      LWF_ST(0)
-      {
-        const int call = ly->call;
-        const int u = call >= 0 ? p->call_u[call] : L;
-        const int sparse = p->prob && call >= 0 && u < L;
-        fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
-              u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
-      }
-      __syncthreads();
-      LWF_ST(1)
-      fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
-      const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
-      __syncthreads();
-      LWF_ST(0)
-      fln<NC>(X, ldD, L, D, n1, X, ldD);
-      __syncthreads();
-      LWF_ST(2)
-      fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
-      __syncthreads();
-      LWF_ST(0)
-      fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
-      const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
-      __syncthreads();
-      LWF_ST(0)
-      fln<NC>(X, ldD, L, D, n2, X, ldD);
-      __syncthreads();
-      LWF_ST(2)
-      if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
-        fgemm<1, FIX ? 64 : 0, FIX ? 192 : 0>(blob, pw, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
-        __syncthreads();
-        LWF_ST(0)
-        const int Lo = ly->Lo;
-        for (int k = tid_op(); k < Lo * D; k += NTH) {
-          const int t = k / D, c = k - t * D;
-          float v = lsm[T + (2 * t) * ldF + c];
-          if (2 * t + 1 < L) v = fmaxf(v, lsm[T + (2 * t + 1) * ldF + c]);
-          if (2 * t - 1 >= 0) v = fmaxf(v, lsm[T + (2 * t - 1) * ldF + c]);
-          lsm[X + t * ldD + c] = v;
-        }
-        __syncthreads();
-        LWF_ST(3)
-        L = Lo;
-      }
+    return Lout;
+  };
+  // the window x[:, -L:] of the embedded input for encoder i > 0
+  auto enc_window = [&](int L) __attribute__((always_inline)) {
+    for (int k = tid_op(); k < L * D; k += NTH) {
+      const int t = k / D, c = k - t * D;
+      lsm[X + t * ldD + c] = lsm[E1 + (e1rows - L + t) * ldD + c];
     }
-    // Encoder.norm → rows [eoff, eoff + L) of the concatenated stack output
+    __syncthreads();
+    LWF_ST(3)
+  };
+  // Encoder.norm → rows [eoff, eoff + L) of the concatenated stack output
+  auto enc_norm = [&](auto Lc, int i) __attribute__((always_inline)) {
+    const int L = Lc;
     fln<NC>(X, ldD, L, D, lnpre<NC>(blob + p->ng[i], blob + p->nb[i], D), ENC + PA(eoff, i) * ldD, ldD);
     __syncthreads();
     LWF_ST(2)
+  };
+  if constexpr (FIX) {
+    // the checkpoint's two encoders: rows 25 → 13 → 7 → 4 and 12 → 6 → 3 (D64Plan, checked by plan_is_d64)
+    enc_layer(ICn<25>{}, 0, 0);
+    enc_layer(ICn<13>{}, 0, 1);
+    enc_layer(ICn<7>{}, 0, 2);
+    enc_layer(ICn<4>{}, 0, 3);
+    enc_norm(ICn<4>{}, 0);
+    enc_window(12);
+    enc_layer(ICn<12>{}, 1, 0);
+    enc_layer(ICn<6>{}, 1, 1);
+    enc_layer(ICn<3>{}, 1, 2);
+    enc_norm(ICn<3>{}, 1);
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < PV(nenc); ++i) {
+      int L = PA(eL0, i);
+      if (i > 0) enc_window(L);
+#pragma unroll 1
+      for (int l = 0; l < PA(nl, i); ++l) L = enc_layer(L, i, l);
+      enc_norm(L, i);
+    }
   }
   // ---- decoder
   {
@@ -642,6 +671,13 @@ bool plan_is_d64(const FPlan& p) {
             p.scr_floats == Q::scr_floats && p.attn_waves == Q::attn_waves && p.lds_floats == Q::lds_floats &&
             p.pred == Q::pred && p.c_out == Q::c_out;
   for (int i = 0; ok && i < Q::nenc; ++i) ok = p.nl[i] == Q::nl[i] && p.eL0[i] == Q::eL0[i] && p.eoff[i] == Q::eoff[i];
+  // every layer but an encoder's last one distils (the instance's compile-time row counts)
+  const int lo[2][4] = {{13, 7, 4, 0}, {6, 3, 0, 0}};
+  for (int i = 0; ok && i < Q::nenc; ++i)
+    for (int l = 0; ok && l < Q::nl[i]; ++l) {
+      const bool conv = l < Q::nl[i] - 1;
+      ok = (p.enc[i][l].conv != 0) == conv && (!conv || p.enc[i][l].Lo == lo[i][l]);
+    }
   return ok;
 }
 
