@@ -1444,10 +1444,24 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen) {
   return (int)e->dbg_json.size();
 }
 
+// The plan is C2's encoder: one encoder of four layers on rows 90 → 45 → 23 → 12, the first three distilling
+// (the v4 kernel's C2 instance takes these row counts as compile-time constants).
+static bool plan_is_c2(const InformerPlan& p) {
+  if (p.n_enc != 1 || p.enc_layers[0] != 4 || p.seq_len != 90) return false;
+  static const int lin[4] = {90, 45, 23, 12}, lout[4] = {45, 23, 12, 12};
+  for (int l = 0; l < 4; ++l) {
+    const auto& d = p.enc[p.enc_first[0] + l];
+    if (d.L_in != lin[l] || d.L_out != lout[l] || (d.conv.n != 0) != (l < 3)) return false;
+  }
+  return true;
+}
+
 static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   const InformerPlan& p = e->ip;
   InformerArgs b = a;
   b.wlo = (uint32_t)(e->wblob.size() * 2);
+  const char* c2env = std::getenv("CET_V4_C2");
+  b.c2 = plan_is_c2(p) && !(c2env && std::strcmp(c2env, "0") == 0);
   b.enc_split = 0;
   b.enc_xchg = nullptr;
   b.enc_count = nullptr;

@@ -17,7 +17,7 @@ namespace v4 {
 
 // P: precision of the dense (LSQ-quantisable) layers; DIAG: the instance that honours the optional
 // outputs (attns maps, activation dumps, phase stamps) — the production instance compiles them out.
-template <int DFF, bool DIAG, int P, bool SPLIT = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false>
 __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(plan))
@@ -183,9 +183,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     STAMP();  // embedding
 
     const int first = PL.enc_first[e];
-    for (int l = 0; l < PL.enc_layers[e]; ++l) {
-      L = ELD.L_in;
-      nmt = (L + 15) >> 4;
+    // one encoder layer on L rows (a compile-time constant in the C2 instance: its tile counts, LayerNorm
+    // bounds and attention dispatch fold); returns the rows leaving its distil conv
+    auto enc_layer = [&](auto Lc, int l) __attribute__((always_inline)) {
+      const int L = Lc;
+      const int nmt = (L + 15) >> 4;
+      int Lout = L;
       // ---- AttentionLayer + ProbAttention / FullAttention, one head per wave, context → CTX
       {
         const GemmDesc q = ELD.qkv;
@@ -255,17 +258,27 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
           }
         });
         FINE(l, 6);
-        L = ELD.L_out;
-        nmt = (L + 15) >> 4;
+        Lout = ELD.L_out;
         __syncthreads();                   // every wave finished reading XB
         FINE(l, 7);
-        store_res(X, nmt, L, XB);
+        store_res(X, (Lout + 15) >> 4, Lout, XB);
         __syncthreads();
         STAMP();  // distil conv + pool
-        if (dbg && ELD.dbg_conv >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_conv);
+        if (dbg && ELD.dbg_conv >= 0) dump_res(X, (Lout + 15) >> 4, Lout, dbg + ELD.dbg_conv);
       }
       (void)last_of_stack;
+      return Lout;
+    };
+    if constexpr (C2) {
+      // C2 (BASELINE configs[1]): one encoder of four layers, rows 90 → 45 → 23 → 12 (launch_v4 checks the plan)
+      enc_layer(IC<90>{}, 0);
+      enc_layer(IC<45>{}, 1);
+      enc_layer(IC<23>{}, 2);
+      L = enc_layer(IC<12>{}, 3);
+    } else {
+      for (int l = 0; l < PL.enc_layers[e]; ++l) L = enc_layer(ELD.L_in, l);
     }
+    nmt = (L + 15) >> 4;
     // ---- Encoder.norm (encoder.py:83-84) → this encoder's rows of the stack output (ENC)
     const int rows = PL.enc_rows[e];
     const Img<P> encw{ENC.base + PL.enc_row_off[e] * G::RS, ENC.lo};
@@ -540,10 +553,10 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 }
 
 // X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
-template <int DFF, bool DIAG, int P, bool SPLIT = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false>
 __global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
     informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
-  informer_forward_v4_body<DFF, DIAG, P, SPLIT>(a, plan);
+  informer_forward_v4_body<DFF, DIAG, P, SPLIT, C2>(a, plan);
 }
 
 template <int P>
@@ -563,6 +576,8 @@ int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream)
     } else {
       return -3;
     }
+  } else if (dff == 64 && a->c2 && !diag && P == P_BF16) {
+    kern = informer_forward_v4<64, false, P, false, true>;   // the C2 plan's compile-time row counts
   } else if (dff == 64) kern = diag ? informer_forward_v4<64, true, P> : informer_forward_v4<64, false, P>;
   else if (dff == 128) kern = diag ? informer_forward_v4<128, true, P> : informer_forward_v4<128, false, P>;
   else return -3;
