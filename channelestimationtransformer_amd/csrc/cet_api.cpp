@@ -1576,6 +1576,8 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     a.out = out;
     a.dbg = e->dbg;
     a.B = B;
+    const char* c3env = std::getenv("CET_V4_C3");
+    a.c3 = e->tp.src_len == 90 && e->tp.tgt_len == 15 && !(c3env && std::strcmp(c3env, "0") == 0);
     const int tk = timing_mark(e, st);
     rc = cet_launch_transformer_v4(&a, e->tcfg.d_ff, e->tp.lds4_bytes, st);
     if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);

@@ -576,7 +576,7 @@ int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream)
     } else {
       return -3;
     }
-  } else if (dff == 64 && a->c2 && !diag && P == P_BF16) {
+  } else if (dff == 64 && a->c2 && !diag && P != P_X3) {
     kern = informer_forward_v4<64, false, P, false, true>;   // the C2 plan's compile-time row counts
   } else if (dff == 64) kern = diag ? informer_forward_v4<64, true, P> : informer_forward_v4<64, false, P>;
   else if (dff == 128) kern = diag ? informer_forward_v4<128, true, P> : informer_forward_v4<128, false, P>;

@@ -78,6 +78,8 @@ struct TransformerArgs {
   float* out;
   float* dbg;
   int B;
+  int c3;   // the plan is C3's (src_len 90, tgt_len 15): the production launch takes the instance with those
+            // lengths at compile time
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize, 160 KiB) for `kern` on the CURRENT device,

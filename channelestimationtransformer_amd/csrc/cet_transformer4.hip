@@ -21,7 +21,7 @@ namespace v4 {
 template <int N>
 using TIC = std::integral_constant<int, N>;
 
-template <int DFF, bool DIAG>
+template <int DFF, bool DIAG, bool C3 = false>
 __global__ void __launch_bounds__(NTHREADS, 4)
     transformer_forward_v4(TransformerArgs a, const TransformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -45,7 +45,8 @@ __global__ void __launch_bounds__(NTHREADS, 4)
   float* XDEC = reinterpret_cast<float*>(lds + v4_enc(P));  // staged x_dec (own region, at entry)
   float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * pl.dbg_stride : nullptr;
 
-  const int C = pl.C, CSH = C == 8 ? 3 : 4, CS = pl.in_stride, L = pl.src_len, Ld = pl.tgt_len;
+  // C3: the BASELINE configuration's lengths (src 90, tgt 15) as compile-time constants (tile loops fold)
+  const int C = pl.C, CSH = C == 8 ? 3 : 4, CS = pl.in_stride, L = C3 ? 90 : pl.src_len, Ld = C3 ? 15 : pl.tgt_len;
   const int t4 = 4 * (int)threadIdx.x;
   f32x4 xe4 = {0.f, 0.f, 0.f, 0.f}, xd4 = xe4;
   if (t4 < L * C) xe4 = *reinterpret_cast<const f32x4*>(a.x_enc + (size_t)b * L * C + t4);
@@ -214,7 +215,8 @@ extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff,
   using K = void (*)(TransformerArgs, const TransformerPlan*);
   K kern = nullptr;
   const bool diag = a->dbg != nullptr;
-  if (dff == 64) kern = diag ? v4::transformer_forward_v4<64, true> : v4::transformer_forward_v4<64, false>;
+  if (dff == 64 && a->c3 && !diag) kern = v4::transformer_forward_v4<64, false, true>;
+  else if (dff == 64) kern = diag ? v4::transformer_forward_v4<64, true> : v4::transformer_forward_v4<64, false>;
   else if (dff == 128) kern = diag ? v4::transformer_forward_v4<128, true> : v4::transformer_forward_v4<128, false>;
   else return -3;
   if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
