@@ -36,7 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
-KERNEL_NAME = "cet::v4::informer_forward_v4<64, false, 0, false>"
+KERNEL_NAME = "cet::v4::informer_forward_v4<64, false, 0, false, true>"   # the C2 instance (plan_is_c2)
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 KALONE = 256                  # back-to-back launches of the kernel-alone timing after the timed loop
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,

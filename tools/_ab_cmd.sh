@@ -1,13 +1,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-L=channelestimationtransformer_amd
-O=gpurun_out/ab18; mkdir -p $O
-CET_LIB=$(pwd)/$L/libcet_c3.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests_c3.log 2>&1 || { tail -30 $O/tests_c3.log; exit 1; }
-echo "c3 $(tail -1 $O/tests_c3.log)"
-for v in base7 c3; do CET_LIB=$(pwd)/$L/libcet_$v.so timeout -k 10 600 python tools/bench_configs.py > $O/configs_$v.jsonl 2> $O/configs_$v.err || { tail -5 $O/configs_$v.err; exit 1; }; echo "== $v"; python - $O/configs_$v.jsonl <<'PY'
-import json,sys
-for l in open(sys.argv[1]):
-    d=json.loads(l); print(d['config'][:40], d['kernel_ms'], d['seq_per_s'], d.get('parity_rel_nmse_vs_oracle'))
-PY
-done
+bash tools/session.sh r04i tests smoke bench1 prof traffic pmcinst pmcwait stamps configs || exit 1
+cp gpurun_out/r04i/pmc_traffic.json profiles/r04/pmc_traffic.json
+timeout -k 10 300 python bench.py > gpurun_out/r04i/bench.json 2> gpurun_out/r04i/bench.err || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r04i/bench_steps20.json 2> gpurun_out/r04i/bench_steps20.err || exit 1
+cut -c1-250 gpurun_out/r04i/bench.json gpurun_out/r04i/bench_steps20.json
 echo done
