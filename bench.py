@@ -36,7 +36,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel-sequences/sec + NMSE(dB), FullPrecision Informer @1/2/4/8 MI355X"
-KERNEL_NAME = "cet::v4::informer_forward_v4<64, false, 0, false, true>"   # the C2 instance (plan_is_c2)
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 KALONE = 256                  # back-to-back launches of the kernel-alone timing after the timed loop
 CFG = dict(enc_in=16, dec_in=16, c_out=16, seq_len=90, label_len=10, pred_len=5, factor=5, d_model=128,
@@ -279,7 +278,6 @@ def main(argv=None):
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.timing(True, every=16)     # HIP events around 1 launch in 16 of lane 0's launches (on its stream)
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k, k)
@@ -288,27 +286,36 @@ def main(argv=None):
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt_rank = time.perf_counter() - t0
-    kern_ms_if, launches_if = eng.timing_read()
-    eng.timing(False)
     last = lanes[(args.steps - 1) % NL]   # the lane that ran the last timed step
     out_last = last["out"].clone()        # its predictions, kept for the collation below
-    # the kernel alone, after the timed loop (roofline.kernel_ms): lane 0's launches back to back on its
-    # stream with nothing else in flight, one event pair around KALONE launches
-    st0 = lanes[0]["stream"]
+    path = eng.last_path()                # the fused kernel the timed steps launched
+    if path != "v4":
+        raise SystemExit(f"the timed steps ran the {path} path, not the fused v4 kernel")
+    kernel_name = eng.last_kernel()       # its instance (the C2 one when the plan is C2's: plan_is_c2)
+    # the kernel alone, after the timed loop (roofline.kernel_ms): lane 0's forward launches back to back on
+    # its stream with nothing else in flight, one event pair around KALONE launches (the forward only: with
+    # --nmse separate the reduction's launch is left out)
+    ln0 = lanes[0]
+    st0 = ln0["stream"]
+
+    def forward_only():
+        if args.nmse == "fused":
+            ln0["fused"](args.steps)
+        else:
+            with torch.cuda.stream(st0):
+                ln0["eng"].forward(ln0["xe"], ln0["xd"], ln0["out"], None, st0.cuda_stream)
     for _ in range(16):   # the clock is still at its loaded level: the timed loop just ended
-        step(-1, 0)
+        forward_only()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     ev0.record(st0)
     for _ in range(KALONE):
-        step(-1, 0)
+        forward_only()
     ev1.record(st0)
     torch.cuda.synchronize(dev)
     kern_ms, launches = ev0.elapsed_time(ev1), KALONE
-    path = eng.last_path()            # the fused kernel the timed steps launched
-    if path != "v4":
-        raise SystemExit(f"the timed steps ran the {path} path, not the fused v4 kernel")
-    kernel_name = KERNEL_NAME
+    if eng.last_kernel() != kernel_name:
+        raise SystemExit(f"the kernel-alone loop ran {eng.last_kernel()}, the timed steps {kernel_name}")
 
     per_rank = [dt_rank]
     if dist:
@@ -376,12 +383,6 @@ def main(argv=None):
                                             "after the timed loop, nothing else in flight, one HIP event pair "
                                             "around them (independent of --steps; compare the rocprofv3 "
                                             "kernel-trace average in profiles/)" % KALONE),
-                         "kernel_ms_in_flight": round(kern_ms_if / max(launches_if, 1), 4),
-                         "kernel_ms_in_flight_note": ("HIP events around 1 in 16 of lane 0's launches during the "
-                                                      "timed loop (%d sampled); with %d batches in flight a "
-                                                      "launch shares the GPU with its neighbours: %.2f x the "
-                                                      "step time" % (launches_if, NL, (kern_ms_if / max(
-                                                          launches_if, 1)) / (dt / args.steps * 1e3))),
                          "achieved_from_throughput": round(flops * seqs / dt / 1e12, 3),
                          "frac_effective": round(flops * seqs / dt / 1e12 / PEAK_BF16_TFLOPS, 5),
                          "flops_per_seq": flops, "io_bytes_per_seq": io_bytes(),

@@ -61,6 +61,7 @@ def _load():
         "cet_timing": (c_int, [c_void_p, c_int]),
         "cet_set_variant": (c_int, [c_void_p, c_int]),
         "cet_last_path": (c_int, [c_void_p]),
+        "cet_last_kernel": (c_int, [c_void_p, c_char_p, c_int]),
         "cet_set_sampler": (c_int, [c_void_p, c_int]),
         "cet_set_precision": (c_int, [c_void_p, c_int]),
         "cet_get_precision": (c_int, [c_void_p]),
@@ -85,7 +86,7 @@ EXPORTED = ("cet_last_error", "cet_version", "cet_create_informer", "cet_create_
             "cet_native_draw", "cet_peek_draw",
             "cet_forward", "cet_forward_nmse", "cet_attns_floats", "cet_attns_layout", "cet_set_debug", "cet_debug_floats",
             "cet_debug_layout", "cet_nmse_split", "cet_nmse_split_sums", "cet_timing", "cet_timing_read",
-            "cet_set_variant", "cet_last_path", "cet_set_sampler", "cet_set_precision", "cet_get_precision", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
+            "cet_set_variant", "cet_last_path", "cet_last_kernel", "cet_set_sampler", "cet_set_precision", "cet_get_precision", "cet_set_stamps", "cet_prepare_batch", "cet_synth_channels")
 
 
 def check(rc: int, what: str = "") -> int:

@@ -135,6 +135,7 @@ struct cet_engine {
   bool dirty = true;
   bool uploaded = false;
   int last_path = 0; // the fused kernel the last forward launched (CET_PATH_*), 0: none yet
+  std::string last_kernel;   // its instance, as rocprofv3 names it (cet_last_kernel)
   bool enc_split_ok = true;   // v4 encoder split allowed (CET_NO_ENC_SPLIT at creation turns it off)
   int variant = 4;   // fused-kernel generation: 4 (one sequence per workgroup), the only one kept
   // shapes outside the fused kernels (d_model != 128, n_heads != 8, d_ff > 128, ...): the layer-wise
@@ -1491,6 +1492,15 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
     b.enc_count = e->d_enc_count;
   }
   e->last_path = split ? CET_PATH_V4_SPLIT : CET_PATH_V4;
+  {
+    // the instance launch_v4 takes (v4_instance: one decision for both sides)
+    const int inst = v4_instance(b, e->prec, e->icfg.d_ff);
+    char nm[160];
+    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %s, %s>", e->icfg.d_ff,
+                  inst == V4I_DIAG ? "true" : "false", e->prec, inst == V4I_SPLIT ? "true" : "false",
+                  inst == V4I_C2 || inst == V4I_C2_STAMPS ? "true" : "false", inst == V4I_C2_STAMPS ? "true" : "false");
+    e->last_kernel = inst == V4I_NONE ? std::string() : std::string(nm);
+  }
   return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);
 }
 
@@ -1540,6 +1550,7 @@ static int forward_lw(cet_engine* e, const float* x_enc, const float* x_dec, int
   const int rc = e->lw->forward(x_enc, x_dec, B, out, attns, e->lw->d_idx, st);
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   e->last_path = e->lw->last_fused ? CET_PATH_LW_FUSED : CET_PATH_LW;
+  e->last_kernel = e->lw->last_fused ? "cet::lw::lw_fused" : "";   // the operator path launches several kernels
   if (rc) return fail(CET_E_HIP, std::string("layer-wise launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (label && cet_launch_nmse_split(out, label, B, e->icfg.out_len, e->icfg.c_out, nmse_acc, nullptr, 1, nmse_sums, st))
     return fail(CET_E_HIP, "nmse launch failed");
@@ -1578,6 +1589,13 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     a.B = B;
     const char* c3env = std::getenv("CET_V4_C3");
     a.c3 = e->tp.src_len == 90 && e->tp.tgt_len == 15 && !(c3env && std::strcmp(c3env, "0") == 0);
+    {
+      const bool tdiag = a.dbg != nullptr, c3 = e->tcfg.d_ff == 64 && a.c3 && !tdiag;
+      char nm[128];
+      std::snprintf(nm, sizeof nm, "cet::v4::transformer_forward_v4<%d, %s, %s>", e->tcfg.d_ff, tdiag ? "true" : "false",
+                    c3 ? "true" : "false");
+      e->last_kernel = nm;
+    }
     const int tk = timing_mark(e, st);
     rc = cet_launch_transformer_v4(&a, e->tcfg.d_ff, e->tp.lds4_bytes, st);
     if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
@@ -1776,6 +1794,12 @@ int cet_set_variant(cet_engine* e, int variant) {
 int cet_last_path(cet_engine* e) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   return e->last_path;
+}
+
+int cet_last_kernel(cet_engine* e, char* name, int buflen) {
+  if (!e) return fail(CET_E_INVALID, "null engine");
+  if (name && buflen > 0) std::snprintf(name, buflen, "%s", e->last_kernel.c_str());
+  return (int)e->last_kernel.size();
 }
 
 int cet_timing(cet_engine* e, int enable) {

@@ -17,7 +17,9 @@ namespace v4 {
 
 // P: precision of the dense (LSQ-quantisable) layers; DIAG: the instance that honours the optional
 // outputs (attns maps, activation dumps, phase stamps) — the production instance compiles them out.
-template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false>
+// ST: a production instance that honours the phase stamps only (the C2 + stamps diagnostic build,
+// -DCET_C2_STAMPS: per-phase cycles of the instance the bench times).
+template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false, bool ST = false>
 __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(plan))
@@ -50,7 +52,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   float* IN = reinterpret_cast<float*>(lds + v4_ctx(P));                // staged raw input (aliases CTX)
   float* dbg = DIAG && a.dbg ? a.dbg + (size_t)b * PL.dbg_stride : nullptr;
 
-  if (DIAG && a.stamps && threadIdx.x == 0) a.stamps[(size_t)b * MAX_STAMPS + 127] = __builtin_amdgcn_s_memtime();
+  if ((DIAG || ST) && a.stamps && threadIdx.x == 0) {
+    a.stamps[(size_t)b * MAX_STAMPS + 127] = __builtin_amdgcn_s_memtime();
+    // the constant 100 MHz clock, comparable across workgroups and XCDs (s_memtime is not)
+    a.stamps[(size_t)b * MAX_STAMPS + 98] = __builtin_amdgcn_s_memrealtime();
+  }
   const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride, Ld = PL.dec_len;
   // this sequence's x_enc rows are requested first (one f32x4 per thread: L·C/4 ≤ 384), so their HBM
   // latency overlaps the LDS zeroing
@@ -83,7 +89,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   if (a.label && t4 < nlab) *reinterpret_cast<f32x4*>(LAB + t4) = lb4;
 
   Res<MT> X;
-  unsigned long long* stamps = DIAG && a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
+  unsigned long long* stamps = (DIAG || ST) && a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
   int sid = 0;
   auto STAMP = [&]() {
     if (stamps) {
@@ -144,15 +150,17 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       if (sparse) io.cnt = CNT;
     }
   };
-  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles (exact: the encoder has
-  // a case for every nmt, the decoder self-attention's bound is its own length)
-  auto attend = [&](auto MQc, auto MKc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
+  // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles; NKXc: whether MKc is
+  // exactly ceil(LK / 16) (true for the encoder, which has a case for every nmt, and for the decoder
+  // self-attention, whose bound is its own length; the un-hoisted cross-attention passes it per bound)
+  auto attend = [&](auto MQc, auto MKc, auto NKXc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
                     uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
                     int mix, int call, float* attn_out) {
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
+    constexpr bool NKX_ = decltype(NKXc)::value;
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
     call_setup(io, call);
-    attention_head<P, MQ_, MK_, false, true>(io, M, w);
+    attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
@@ -193,7 +201,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       {
         const GemmDesc q = ELD.qkv;
         auto enc_attend = [&](auto NQ) __attribute__((always_inline)) {
-          attend(NQ, NQ, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
+          attend(NQ, NQ, std::true_type{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
                  part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
                  DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
         };
@@ -365,7 +373,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       {
         // masked self-attention with the mix scramble (model.py:211-222)
         const GemmDesc q = DLD.qkv;
-        attend(IC<NMD>{}, IC<NMD>{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+        attend(IC<NMD>{}, IC<NMD>{}, std::true_type{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
                part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld, PL.prob, 1, PL.mix, DLD.call, nullptr);
       }
       const WPre<P, 4> po = prefetch_res<P, 4>(M, DLD.o);
@@ -388,7 +396,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         attention_head<P, NMD, NMS, true, NMS == 1>(cio, M, w, CK, CV, cqp);
 #else
         const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
-        attend(IC<NMD>{}, IC<NMS>{}, XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+        // the key-tile bound MT is exact only for S in 81-96; NMS == 1 is exact (S ≤ 16)
+        attend(IC<NMD>{}, IC<NMS>{}, std::bool_constant<NMS == 1>{}, XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
                part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
 #endif
       }
@@ -462,6 +471,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       if (fuse) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done
     }
     STAMP();  // final norm + projection
+    if (stamps && threadIdx.x == 0) stamps[99] = __builtin_amdgcn_s_memrealtime();
   };
   switch ((Ld + 15) >> 4) {
     case 1: S <= 16 ? decoder(IC<1>{}, IC<1>{}) : decoder(IC<1>{}, IC<MT>{}); break;
@@ -553,34 +563,35 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 }
 
 // X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false, bool ST = false>
 __global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
     informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
-  informer_forward_v4_body<DFF, DIAG, P, SPLIT, C2>(a, plan);
+  informer_forward_v4_body<DFF, DIAG, P, SPLIT, C2, ST>(a, plan);
 }
 
 template <int P>
 int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
   if (a->B <= 0) return 0;
-  const bool diag = a->attns || a->dbg || a->stamps;
   using K = void (*)(InformerArgs, const InformerPlan*);
   K kern = nullptr;
   const bool split = a->enc_split != 0;
-  if (split) {
-    // encoder split: bf16 policy, production instance only (the launcher checks the plan's conditions)
-    if constexpr (P == P_BF16) {
-      if (diag) return -3;
-      if (dff == 64) kern = informer_forward_v4<64, false, P, true>;
-      else if (dff == 128) kern = informer_forward_v4<128, false, P, true>;
-      else return -3;
-    } else {
-      return -3;
-    }
-  } else if (dff == 64 && a->c2 && !diag && P != P_X3) {
-    kern = informer_forward_v4<64, false, P, false, true>;   // the C2 plan's compile-time row counts
-  } else if (dff == 64) kern = diag ? informer_forward_v4<64, true, P> : informer_forward_v4<64, false, P>;
-  else if (dff == 128) kern = diag ? informer_forward_v4<128, true, P> : informer_forward_v4<128, false, P>;
-  else return -3;
+  switch (v4_instance(*a, P, dff)) {
+    case V4I_SPLIT:   // encoder split: bf16 policy, production instance only (the launcher checks the plan)
+      if constexpr (P == P_BF16) kern = dff == 64 ? informer_forward_v4<64, false, P, true> : informer_forward_v4<128, false, P, true>;
+      break;
+#ifdef CET_C2_STAMPS
+    case V4I_C2_STAMPS:   // C2 instance + phase stamps (diagnostic build)
+      if constexpr (P == P_BF16) kern = informer_forward_v4<64, false, P, false, true, true>;
+      break;
+#endif
+    case V4I_C2:
+      if constexpr (P != P_X3) kern = informer_forward_v4<64, false, P, false, true>;
+      break;
+    case V4I_DIAG: kern = dff == 64 ? informer_forward_v4<64, true, P> : informer_forward_v4<128, true, P>; break;
+    case V4I_GENERIC: kern = dff == 64 ? informer_forward_v4<64, false, P> : informer_forward_v4<128, false, P>; break;
+    default: break;
+  }
+  if (!kern) return -3;
   if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
   InformerArgs args = *a;
   args.lds_bytes = lds_bytes;

@@ -42,6 +42,20 @@ struct InformerArgs {
                               // bf16 production launch takes the instance with those rows at compile time
 };
 
+// The v4 Informer instance a launch takes.  launch_v4 (cet_informer4.hpp) launches exactly this choice and
+// the host reports it (cet_last_kernel), so the two agree by construction.  prec: 0 bf16, 1 split bf16, 2 fp8.
+enum V4Instance { V4I_NONE = 0, V4I_GENERIC = 1, V4I_DIAG = 2, V4I_C2 = 3, V4I_SPLIT = 4, V4I_C2_STAMPS = 5 };
+__host__ __device__ inline int v4_instance(const InformerArgs& a, int prec, int dff) {
+  const bool diag = a.attns || a.dbg || a.stamps;
+  if (dff != 64 && dff != 128) return V4I_NONE;
+  if (a.enc_split) return prec == 0 && !diag ? V4I_SPLIT : V4I_NONE;   // bf16 production only
+#ifdef CET_C2_STAMPS
+  if (dff == 64 && a.c2 && a.stamps && !a.attns && !a.dbg && prec == 0) return V4I_C2_STAMPS;
+#endif
+  if (dff == 64 && a.c2 && !diag && prec != 1) return V4I_C2;   // the C2 plan's compile-time row counts
+  return diag ? V4I_DIAG : V4I_GENERIC;
+}
+
 // device channel pipeline (cet_data.hip)
 struct PrepArgs {
   const float2* dataset;   // [n_samples][slots][E] complex64, E = Nr·Nt

@@ -63,7 +63,7 @@ int Model::build_fused() {
   if (Lm > F_LMAX || S > F_LMAX || S < 1) return 0;
   // the validated range (tests/test_gpu_layerwise.py: up to 48 rows = 3 m-tiles, d_model ≤ 256 for the
   // 16-lane LayerNorm rows); wider shapes keep the operator launches
-  if (Lm > 48 || D > 256) return 0;
+  if (Lm > 48 || S > 48 || D > 256) return 0;   // S: the cross-attention K/V GEMM runs over S rows
   for (const auto& e : enc)
     if ((int)e.size() > F_MAX_EL) return 0;
   auto r16 = [](int x) { return (x + 15) & ~15; };

@@ -204,6 +204,14 @@ class Engine:
         launches), "layerwise-fused" (the layer-wise forward in one launch) or None."""
         return self.PATHS[check(lib.cet_last_path(self._h), "cet_last_path")]
 
+    def last_kernel(self) -> str:
+        """The kernel instance the last forward launched, as rocprofv3 names it (include/cet.h
+        cet_last_kernel), e.g. "cet::v4::informer_forward_v4<64, false, 0, false, true, false>" (C2)."""
+        n = check(lib.cet_last_kernel(self._h, None, 0), "cet_last_kernel")
+        buf = ctypes.create_string_buffer(n + 1)
+        check(lib.cet_last_kernel(self._h, buf, n + 1), "cet_last_kernel")
+        return buf.value.decode()
+
     PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3}
 
     def set_precision(self, prec) -> None:

@@ -129,6 +129,12 @@ int cet_set_variant(cet_engine* e, int variant);
  * per sequence with its activations in LDS), 0 before any. */
 enum { CET_PATH_LW = 3, CET_PATH_V4 = 4, CET_PATH_LW_FUSED = 31, CET_PATH_V4_SPLIT = 41 };
 int cet_last_path(cet_engine* e);
+/* The kernel instance the engine's last forward launched, as rocprofv3's kernel trace names it (e.g.
+ * "cet::v4::informer_forward_v4<64, false, 0, false, true, false>" for the C2 instance: d_ff, diagnostic
+ * outputs, precision, encoder split, C2 compile-time rows, phase stamps), written NUL-terminated into
+ * name[buflen]; returns its length (0 before any forward, or after a layer-wise forward of several
+ * operator launches).  No reference counterpart: measurement plumbing (bench.py's roofline.kernel). */
+int cet_last_kernel(cet_engine* e, char* name, int buflen);
 
 /* Operand precision of the v4 kernel's dense layers (Informer engines):
  *   -1 auto (default): 0, or 1 where bf16 cannot carry the model — an LSQ integer grid with |q| > 256,

@@ -707,3 +707,70 @@ def test_fused_nmse_odd_batch_and_label_width(c_out):
     torch.cuda.synchronize()
     assert eng.last_path() == "v4"
     np.testing.assert_allclose((s[0] / s[1]).cpu().numpy(), ref_split(o.cpu().numpy(), lab_np), rtol=1e-5)
+
+
+C2_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, true, false>"
+
+
+def _c2_model(attn, seed, bias_offset=0.0):
+    """The C2 architecture (e_layers [4], distil, seq_len 90) with seeded synthetic weights; bias_offset is
+    added to every attention out-projection bias, so every LN1 input row carries that mean offset."""
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+
+    dev = torch.device("cuda:0")
+    m = InformerStack(16, 16, 16, 90, 10, 5, 5, 128, 8, [4], 3, 64, 0.05, attn, "fixed", "gelu", False, True, dev)
+    sd = synthetic_state_dict(m._schema(), seed)
+    if bias_offset:
+        sd = {k: (np.asarray(v) + np.float32(bias_offset) if k.endswith("out_projection.bias") else v)
+              for k, v in sd.items()}
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    return m.eval()
+
+
+@pytest.mark.parametrize("attn", ["full", "prob"])
+def test_c2_instance_on_every_plan_it_accepts(attn):
+    """plan_is_c2 (cet_api.cpp) routes every plan with C2's encoder rows (one encoder, 90 → 45 → 23 → 12, the
+    first three layers distilling) to the compile-time C2 instance, whatever the attention: attn="full"
+    (FullAttention in every layer, attn.py:37-70; PL.prob is a runtime flag inside the instance) as well as
+    "prob".  B = 512 against the float64 oracle on a row slice, and the instance asserted by name."""
+    _gpu()
+    from engine_util import run_engine
+
+    from channelestimationtransformer_amd.dataset import make_batch
+    from channelestimationtransformer_amd.rng import draw_indices
+    from oracle.informer_np import InformerConfig, InformerOracle, sample_shapes
+
+    m = _c2_model(attn, 6)
+    cfg = InformerConfig(attn=attn)
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    idx = draw_indices(sample_shapes(cfg), seed=21) if attn == "prob" else None
+    xe, xd, _ = make_batch(512, seed=88)
+    out, _, _ = run_engine(m, xe, xd, idx)
+    eng = m.engine(torch.device("cuda:0"))
+    assert eng.last_path() == "v4"
+    assert eng.last_kernel() == C2_KERNEL
+    rows = np.r_[0:16, 496:512]
+    ref, _ = InformerOracle(cfg, state).forward(xe[rows], xd[rows], idx if idx is not None else ())
+    assert rel_nmse(out[rows], ref) < TOL, rel_nmse(out[rows], ref)
+
+
+@pytest.mark.parametrize("offset", [1e2, 3e2])
+def test_layernorm_rows_with_a_large_mean_offset(offset):
+    """LayerNorm rows whose mean is far above their spread (every attention out-projection bias shifted by
+    `offset`, so each LN1 input row has mean ≈ offset and std ≈ 1): the one-pass (Σx, Σx²) statistics of
+    ln_res must still meet the north star's 1e-4 against the float64 oracle (encoder.py:49-50, decoder.py:
+    31-33; torch.nn.LayerNorm's biased variance).  C2 architecture, attn="full", B = 64."""
+    _gpu()
+    from engine_util import run_engine
+
+    from channelestimationtransformer_amd.dataset import make_batch
+    from oracle.informer_np import InformerConfig, InformerOracle
+
+    m = _c2_model("full", 7, bias_offset=offset)
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    xe, xd, _ = make_batch(64, seed=90)
+    out, _, _ = run_engine(m, xe, xd)
+    assert m.engine(torch.device("cuda:0")).last_kernel() == C2_KERNEL
+    ref, _ = InformerOracle(InformerConfig(attn="full"), state).forward(xe, xd, ())
+    assert rel_nmse(out, ref) < TOL, rel_nmse(out, ref)

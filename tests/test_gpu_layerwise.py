@@ -299,3 +299,35 @@ def test_fused_layerwise_longer_shapes_vs_oracle(attn, seq_len, label_len, pred_
     finally:
         del os.environ["CET_LW_FUSED"]
     assert rel_nmse(out, out2) < 1e-10, rel_nmse(out, out2)
+
+
+@pytest.mark.parametrize("seq_len,path", [(32, "layerwise-fused"), (48, "layerwise")])
+def test_fused_layerwise_stack_output_rows_bound(seq_len, path):
+    """The fused layer-wise GEMM covers at most 3 m-tiles (48 rows), and the decoder's cross-attention K/V
+    GEMM runs over S = the stack output's rows.  e_layers [1, 1] (no distil conv in a one-layer encoder,
+    encoder.py:95-106) gives S = seq_len + seq_len/2: 48 at seq_len 32 (fused), 72 at seq_len 48, which
+    must take the operator launches.  Seeded synthetic weights, d_model 64 (layer-wise shapes), attn
+    "full", against the float64 oracle."""
+    _gpu()
+    from channelestimationtransformer_amd.dataset import make_batch
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+    from oracle.informer_np import InformerConfig, InformerOracle
+
+    dev = torch.device("cuda:0")
+    m = InformerStack(16, 16, 16, seq_len, 10, 5, 5, 64, 4, [1, 1], 2, 64, 0.05, "full", "fixed", "gelu", False,
+                      True, dev)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(m._schema(), 4).items()})
+    m.eval()
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    orc = InformerOracle(InformerConfig(seq_len=seq_len, d_model=64, n_heads=4, e_layers=(1, 1), d_layers=2,
+                                        attn="full"), state)
+    B = 21
+    xe, xd, _ = make_batch(B, seed=41)
+    xe = np.ascontiguousarray(xe[:, -seq_len:])
+    with torch.no_grad():
+        res = m(torch.from_numpy(xe).to(dev), range(seq_len), torch.from_numpy(xd).to(dev), range(15))
+    out = (res[0] if isinstance(res, tuple) else res).cpu().numpy()
+    assert m.engine(dev).last_path() == path
+    ref, _ = orc.forward(xe, xd, ())
+    assert rel_nmse(out, ref) < TOL, rel_nmse(out, ref)

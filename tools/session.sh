@@ -10,6 +10,8 @@
 #   pmcvalu    VALU instructions by kind (float add/mul/fma/transcendental, conversions, integer)
 #   traffic    FETCH_SIZE and WRITE_SIZE passes -> traffic.json
 #   stamps     DIAG per-phase stamps at B=512         configs  tools/bench_configs.py
+#   stampsc2   C2-instance per-phase stamps at B=512 (libcet_c2st.so: make OUT=../libcet_c2st.so
+#              B=build_c2st EXTRA=-DCET_C2_STAMPS)
 #   list       rocprofv3 -L (counter names)
 # CET_LIB in the environment selects an A/B build of the engine for every step.
 set -o pipefail
@@ -66,6 +68,10 @@ for s in "$@"; do
     stamps)
       $T 200 python tools/stamps.py 512 > "$O/stamps_b512.txt" 2> "$O/stamps.err" || { tail -20 "$O/stamps.err"; exit 1; }
       cat "$O/stamps_b512.txt" ;;
+    stampsc2)
+      CET_LIB=$R/channelestimationtransformer_amd/libcet_c2st.so $T 200 python tools/stamps.py 512 \
+        > "$O/stamps_c2_b512.txt" 2> "$O/stampsc2.err" || { tail -20 "$O/stampsc2.err"; exit 1; }
+      cat "$O/stamps_c2_b512.txt" ;;
     configs)
       $T 600 python tools/bench_configs.py > "$O/configs.jsonl" 2> "$O/configs.err" || { tail -5 "$O/configs.err"; exit 1; }
       cut -c1-300 "$O/configs.jsonl" ;;

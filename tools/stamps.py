@@ -1,6 +1,11 @@
-"""Per-phase cycle breakdown of the fused kernel (DIAG instance) from in-kernel s_memtime stamps.
+"""Per-phase cycle breakdown of the fused kernel from in-kernel s_memtime stamps.
 
-Usage (GPU box): python tools/stamps.py [B] [variant] > gpurun_out/stamps.txt
+The stamps run in the DIAG instance, or — in a library built with -DCET_C2_STAMPS (tools/session.sh
+builds it as libcet_c2st.so) — in the C2 production instance the bench times.  Phase durations are
+s_memtime differences inside one workgroup; workgroup start / end offsets come from s_memrealtime
+(the constant 100 MHz clock, comparable across workgroups and XCDs — s_memtime is not).
+
+Usage (GPU box): python tools/stamps.py [B] > gpurun_out/stamps.txt
 """
 import os
 import sys
@@ -26,8 +31,6 @@ def main():
     dev = torch.device("cuda:0")
     m = bench.build_model(dev)
     eng = m.engine(dev)
-    if len(sys.argv) > 2:
-        eng.set_variant(int(sys.argv[2]))
     eng.seed(1)
     xe, xd, _ = make_batch(B, seed=5)
     xe = torch.from_numpy(xe).to(dev)
@@ -43,16 +46,22 @@ def main():
     s = st.view(B, 128).cpu().numpy().astype(np.int64)
     rows = s[:, 0] != 0        # v5 stamps each workgroup (two sequences) in its first sequence's row
     s = s[rows]
-    print(f"kernel path: {eng.last_path()}  stamped workgroups: {int(rows.sum())}")
+    print(f"kernel path: {eng.last_path()}  instance: {eng.last_kernel()}  stamped workgroups: {int(rows.sum())}")
     n = len(NAMES)
     s = s[:, :n]
     d = np.diff(s, axis=1)
     tot = s[:, -1] - s[:, 0]
     print(f"B={B}  per-WG total cycles: mean {tot.mean():.0f}  min {tot.min()}  max {tot.max()}")
-    start = s[:, 0] - s[:, 0].min()
-    print(f"WG start offsets (cycles): median {np.median(start):.0f}  max {start.max()}  "
-          f"WGs starting after 50% of the kernel: {(start > 0.5 * (s[:, -1].max() - s[:, 0].min())).sum()}")
     sub = st.view(B, 128).cpu().numpy().astype(np.int64)[rows]
+    rt0, rt1 = sub[:, 98], sub[:, 99]
+    if rt0.all() and rt1.all():
+        # s_memrealtime: 100 MHz, one clock for the whole chip
+        span = (rt1.max() - rt0.min()) / 100.0
+        start, end = (rt0 - rt0.min()) / 100.0, (rt1 - rt0.min()) / 100.0
+        clk = (s[:, -1] - sub[:, 127]) / ((rt1 - rt0) / 100.0) / 1e3   # GHz: s_memtime ticks per realtime us
+        print(f"kernel span (first WG start -> last WG end): {span:.2f} us;  WG start offsets: median "
+              f"{np.median(start):.2f} us, max {start.max():.2f} us;  WG end: median {np.median(end):.2f} us, "
+              f"min {end.min():.2f} us;  in-kernel clock (memtime/realtime): median {np.median(clk):.3f} GHz")
     SUBN = ["K/V projection", "Q projection", "phase A (M)", "top-u select", "phase C (softmax·V)", "phase D (rest)"]
     for c, base in ((0, 100), (1, 108)):
         ss = sub[:, base:base + 7]
