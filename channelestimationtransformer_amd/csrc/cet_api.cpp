@@ -1463,6 +1463,8 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   b.wlo = (uint32_t)(e->wblob.size() * 2);
   const char* c2env = std::getenv("CET_V4_C2");
   b.c2 = plan_is_c2(p) && !(c2env && std::strcmp(c2env, "0") == 0);
+  b.stagger = 0;
+  if (const char* sg = std::getenv("CET_STAGGER")) b.stagger = std::atoi(sg);
   b.enc_split = 0;
   b.enc_xchg = nullptr;
   b.enc_count = nullptr;

@@ -33,6 +33,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   const int my_e = SPLIT ? (int)blockIdx.x - b * nsplit : -1;   // the one encoder of this workgroup
   if (b >= a.B) return;
   const int w = wave_id();
+#ifdef CET_STAGGER
+  // experiment: CET_STAGGER = mask·65536 + units: workgroups with (b & mask) != 0 idle units·64 cycles first
+  if (a.stagger && (b & (a.stagger >> 16))) {
+    for (int i = 0; i < (a.stagger & 0xffff); ++i) __builtin_amdgcn_s_sleep(1);
+  }
+#endif
 #ifdef CET_SETPRIO
   // static priority for the younger half of the workgroup, the SIMD arbitration loser
   // (MI355X_MICROARCH "Two waves per SIMD" item 4): −0.7 µs at C2 with one batch in flight in round 2
@@ -80,13 +86,69 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       for (int j = 0; j < 4; ++j) lb4[j] = t4 + j < nlab ? lp[j] : 0.f;
     }
   }
+  // C2 with prepared (or host-staged) multiplicity tables: the first sparse call's table is requested with
+  // the inputs at entry and stored into CNT with them, instead of a global copy + barrier at the head of the
+  // first attention phase (104.4 vs 105.4 us kernel alone; staging calls 1-2's tables the same way during
+  // the first layer's FFN / distil phases measured slower: DESIGN §3.0e).
+#ifndef CET_NO_TAB_PRE
+  constexpr bool PRE = C2;
+#else
+  constexpr bool PRE = false;
+#endif
+  f32x4 t0a = {0.f, 0.f, 0.f, 0.f}, t0b = t0a;
+  int t0n = 0;   // 16-byte pieces of call 0's table (≤ 96 rows × 96 B = 576)
+  if constexpr (PRE) {
+    const int c0 = PL.enc[PL.enc_first[0]].call;
+    if (a.cnt && c0 >= 0 && PL.calls[c0].u < PL.calls[c0].LQ) {
+      t0n = ((PL.calls[c0].LQ + 15) & ~15) * PL.calls[c0].cnt_stride / 16;
+      const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + PL.calls[c0].cnt_off);
+      const int i = tid_op();
+      if (i < t0n) t0a = src[i];
+      if (i + NTHREADS < t0n) t0b = src[i + NTHREADS];
+    }
+  }
+#ifdef CET_ZERO_ALL
   // zero the activation images: rows past L are read (never used) by MFMAs
   for (int i = threadIdx.x; i < PL.lds4_zero / 16; i += NTHREADS)
     reinterpret_cast<f32x4*>(lds)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();   // zeroing done before the staged rows land in CTX
+#else
+  {
+    // Zero only the rows an MFMA can read before anything writes them: XB and CTX past the first window this
+    // workgroup embeds (rows L .. LMAX, L = seq_len, or its encoder's window under the encoder split, where no
+    // earlier encoder wrote the rows below L0) and the stack output's padded rows (ENC rows S .. 16·⌈S/16⌉),
+    // every plane.  Padded key / value rows must be finite (one NaN key row reaches every query through the
+    // softmax); the rows below L are written by the first layer before any later layer or the decoder reads
+    // them.  No barrier: the staged rows below land in other bytes (IN rows are 4·in_stride < RS bytes
+    // apart), and the encoder loop's barrier orders both before any reader.
+    constexpr int RS = G::RS, RQ = RS / 16;   // 16-byte slots per image row
+    static_assert(RS % 16 == 0, "image rows of whole 16-byte slots");
+    const int r0 = SPLIT ? L0 >> my_e : L0, S0 = PL.S;
+    const int n_x = (LMAX - r0) * RQ, n_e = (((S0 + 15) & ~15) - S0) * RQ;   // slots per plane
+    const int per = 2 * n_x + n_e;
+    char* const enc0 = lds + v4_enc(P);
+    for (int i = tid_op(); i < G::PLANES * per; i += NTHREADS) {
+      const int pl = i >= per, j = i - pl * per;
+      char* q = j < n_x       ? lds + V4L_XB + pl * G::IMG + r0 * RS + j * 16
+                : j < 2 * n_x ? lds + v4_ctx(P) + pl * G::IMG + r0 * RS + (j - n_x) * 16
+                              : enc0 + pl * PL.lds4_enc_lo + S0 * RS + (j - 2 * n_x) * 16;
+      *reinterpret_cast<f32x4*>(q) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#endif
   if (t4 < L0 * C) *reinterpret_cast<f32x4*>(IN + (t4 >> PL.C_shift) * CS + (t4 & (C - 1))) = xe4;
   if (xdec_off >= 0 && t4 < Ld * C) *reinterpret_cast<f32x4*>(XDEC + (t4 >> PL.C_shift) * CS + (t4 & (C - 1))) = xd4;
   if (a.label && t4 < nlab) *reinterpret_cast<f32x4*>(LAB + t4) = lb4;
+  if constexpr (PRE) {
+    f32x4* dst = reinterpret_cast<f32x4*>(CNT);
+    const int i = tid_op();
+    if (i < t0n) dst[i] = t0a;
+    if (i + NTHREADS < t0n) dst[i + NTHREADS] = t0b;
+  }
+  auto pre_table = [&](int l) -> const uint8_t* {   // the pre-staged table of encoder layer l's call, or null
+    if constexpr (!PRE) return nullptr;
+    return l == 0 && t0n ? CNT : nullptr;
+  };
 
   Res<MT> X;
   unsigned long long* stamps = (DIAG || ST) && a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
@@ -119,7 +181,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     return io;
   };
   // the ProbSparse draws of one attention call: u, the multiplicity table (replayed in-kernel or staged)
-  auto call_setup = [&](HeadIO<P>& io, int call) __attribute__((always_inline)) {
+  auto call_setup = [&](HeadIO<P>& io, int call, const uint8_t* pre) __attribute__((always_inline)) {
 #ifndef CET_STAMP_DEC_CALL
     io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
 #else   // diagnostic: sub-phases of the first encoder call and the first decoder self-attention call
@@ -136,6 +198,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         mt_replay<NTHREADS>(gen, c.LQ, c.U, c.LK, sparse ? reinterpret_cast<uint32_t*>(CNT) : nullptr,
                             c.cnt_stride);
         if (call == PL.n_calls - 1 && b == 0) mt_store<NTHREADS>(gen, a.mt_out);
+      } else if (sparse && pre) {
+        // staged earlier (C2): already in LDS behind an earlier barrier
       } else if (sparse) {
         const int bytes = ((c.LQ + 15) & ~15) * c.cnt_stride;
         const f32x4* src = reinterpret_cast<const f32x4*>(a.cnt + c.cnt_off);
@@ -147,7 +211,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         (void)bytes; (void)src; (void)dst;   // ablation (wrong results)
 #endif
       }
-      if (sparse) io.cnt = CNT;
+      if (sparse) io.cnt = a.cnt && pre ? pre : CNT;
     }
   };
   // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles; NKXc: whether MKc is
@@ -155,26 +219,46 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   // self-attention, whose bound is its own length; the un-hoisted cross-attention passes it per bound)
   auto attend = [&](auto MQc, auto MKc, auto NKXc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
                     uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
-                    int mix, int call, float* attn_out) {
+                    int mix, int call, float* attn_out, const uint8_t* pre = nullptr) {
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     constexpr bool NKX_ = decltype(NKXc)::value;
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
-    call_setup(io, call);
+    call_setup(io, call, pre);
     attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
     if (SPLIT && e != my_e) continue;   // the entry staging of x_enc is still intact for it
     if (!SPLIT && e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);   // CTX was reused by encoder e-1
-    __syncthreads();
-    if (stamps && e == 0 && threadIdx.x == 0) stamps[124] = __builtin_amdgcn_s_memtime();
     // ---- DataEmbedding (embed.py:132-135) on the EncoderStack window x[:, -L:] (encoder.py:95-106)
     int L = L0 >> e;
     const int off = L0 - L;
     int nmt = (L + 15) >> 4;
+#ifndef CET_NO_EMB_PRE
+    // its operands (weight fragments, epilogue vectors, positional rows) requested before the barrier that
+    // publishes the staged input: one L2 round trip under the barrier instead of one per m-tile after it
+    const WPre<PP, 2> pemb = prefetch_res<PP, 2>(M, PL.emb_enc);
+    f32x4 pe[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      pe[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (mt < nmt) {
+        const int lane = lane_op();
+        const int m = mt * 16 + (lane & 15);
+        const int prow = m + off < LMAX ? m + off : LMAX - 1;
+        pe[mt] = pload4(M, PL.pe_enc, prow * DMODEL + 16 * w + (lane >> 4) * 4);
+      }
+    }
+#endif
+    __syncthreads();
+    if (stamps && e == 0 && threadIdx.x == 0) stamps[124] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) X.v[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
+#ifndef CET_NO_EMB_PRE
+      gemm_res<PP, 2, MT>(pemb, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, off},
+                          [&](int mt, int n0, f32x4 y) { X.v[mt] = y + pe[mt]; });
+#else
       const GemmDesc d = PL.emb_enc;
       auto emb_epi = [&](int mt, int n0, f32x4 y) {
         const int m = mt * 16 + (lane_op() & 15);
@@ -182,9 +266,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         X.v[mt] = y + pload4(M, PL.pe_enc, prow * DMODEL + n0);
       };
       gemm_res<PP, 2, MT>(M, d, nmt, LoadEmbed<PP>{IN, L0, PL.C_shift, CS, off}, emb_epi);
+#endif
     }
     if (stamps && e == 0 && threadIdx.x == 0) stamps[125] = __builtin_amdgcn_s_memtime();
-    __syncthreads();                       // IN (aliases CTX) fully read
+#ifdef CET_EMB_BARRIER2
+    __syncthreads();   // (not needed: the embedding reads IN in CTX, the store below writes XB)
+#endif
     store_res(X, nmt, L, XB);
     __syncthreads();
     if (dbg && e == 0) dump_res(X, nmt, L, dbg + PL.dbg_emb);
@@ -203,7 +290,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         auto enc_attend = [&](auto NQ) __attribute__((always_inline)) {
           attend(NQ, NQ, std::true_type{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
                  part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
-                 DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr);
+                 DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr,
+                 pre_table(l));
         };
         switch (nmt) {
           case 1: enc_attend(IC<1>{}); break;

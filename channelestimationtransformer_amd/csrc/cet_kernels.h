@@ -38,6 +38,8 @@ struct InformerArgs {
   int enc_split;              // 0 / 1
   uint64_t* enc_xchg;         // [B][S rows][row stride / 8] bf16 stack-output image rows
   unsigned* enc_count;        // [B] arrivals (the last arrival re-arms it)
+  int stagger;                // experiment (CET_STAGGER=mask:units): workgroups with (b & mask) != 0 sleep units·64
+                              // cycles at entry (-DCET_STAGGER builds only)
   int c2;                     // the plan is C2's encoder (one encoder, rows 90 → 45 → 23 → 12): the
                               // bf16 production launch takes the instance with those rows at compile time
 };

@@ -229,6 +229,9 @@ struct Img : ImgBase<P> {
   __device__ __forceinline__ Img() = default;
   __device__ __forceinline__ XF<P> ld(int row, int k0) const {
     constexpr int RS = Geo<P>::RS;
+#ifdef CET_ABL_LDSROW
+    row &= ~15;   // ablation (wrong results): every lane group reads one row — conflict-free, same instructions
+#endif
     XF<P> r;
     if constexpr (P == P_FP8) {
 #ifdef CET_FP8_SCALED

@@ -49,8 +49,12 @@ for s in "$@"; do
         python "$R/bench.py" --no-cpu-baseline > "$R/$O/bench_under_rocprof.json" 2> "$R/$O/prof_if2.err") \
         || { tail -20 "$O/prof_if2.err"; exit 1; }
       find "$O/prof_if2" -name "*kernel_stats.csv" -exec cut -c1-220 {} \; | head -5 ;;
-    pmcwait|pmcinst|pmcmix|pmcvalu)
+    pmcwait|pmcinst|pmcmix|pmcvalu|pmcbusy|pmcic|pmcic2|pmclds)
       case $s in
+        pmcbusy) C="SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_IFETCH SQ_IFETCH_LEVEL GRBM_GUI_ACTIVE" ;;
+        pmcic) C="SQC_ICACHE_HITS SQC_ICACHE_MISSES" ;;
+        pmcic2) C="SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ" ;;
+        pmclds) C="SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_LDS" ;;
         pmcwait) C="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" ;;
         pmcinst) C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT" ;;
         pmcmix) C="SQ_WAVES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_ACTIVE_INST_FLAT" ;;
