@@ -1445,24 +1445,34 @@ int cet_debug_layout(cet_engine* e, char* json, int buflen) {
   return (int)e->dbg_json.size();
 }
 
-// The plan is C2's encoder: one encoder of four layers on rows 90 → 45 → 23 → 12, the first three distilling
-// (the v4 kernel's C2 instance takes these row counts as compile-time constants).
-static bool plan_is_c2(const InformerPlan& p) {
-  if (p.n_enc != 1 || p.enc_layers[0] != 4 || p.seq_len != 90) return false;
-  static const int lin[4] = {90, 45, 23, 12}, lout[4] = {45, 23, 12, 12};
-  for (int l = 0; l < 4; ++l) {
-    const auto& d = p.enc[p.enc_first[0] + l];
-    if (d.L_in != lin[l] || d.L_out != lout[l] || (d.conv.n != 0) != (l < 3)) return false;
+// The plan's compile-time instance (cet_kernels.h V4Shape): C2's encoder — one encoder of four layers on rows
+// 90 → 45 → 23 → 12, the first three distilling — or the TimingAnalysis stack e_layers [4, 3] — that encoder and
+// one on the window x[:, -45:] (45 → 23 → 12, the first two distilling), 24 stack rows, a decoder of ≤ 16 rows.
+static bool encoder_rows_are(const InformerPlan& p, int e, int n, const int* lin, const int* lout) {
+  if (p.enc_layers[e] != n) return false;
+  for (int l = 0; l < n; ++l) {
+    const auto& d = p.enc[p.enc_first[e] + l];
+    if (d.L_in != lin[l] || d.L_out != lout[l] || (d.conv.n != 0) != (l < n - 1)) return false;
   }
   return true;
+}
+static int plan_shape(const InformerPlan& p) {
+  static const int lin4[4] = {90, 45, 23, 12}, lout4[4] = {45, 23, 12, 12};
+  static const int lin3[3] = {45, 23, 12}, lout3[3] = {23, 12, 12};
+  if (p.seq_len != 90) return V4S_GENERIC;
+  if (p.n_enc == 1 && encoder_rows_are(p, 0, 4, lin4, lout4)) return V4S_C2;
+  if (p.n_enc == 2 && encoder_rows_are(p, 0, 4, lin4, lout4) && encoder_rows_are(p, 1, 3, lin3, lout3) && p.S == 24 &&
+      p.dec_len <= 16)
+    return V4S_E43;
+  return V4S_GENERIC;
 }
 
 static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   const InformerPlan& p = e->ip;
   InformerArgs b = a;
   b.wlo = (uint32_t)(e->wblob.size() * 2);
-  const char* c2env = std::getenv("CET_V4_C2");
-  b.c2 = plan_is_c2(p) && !(c2env && std::strcmp(c2env, "0") == 0);
+  const char* c2env = std::getenv("CET_V4_C2");   // "0": the generic instance for every plan (A/B)
+  b.shape = c2env && std::strcmp(c2env, "0") == 0 ? V4S_GENERIC : plan_shape(p);
   b.stagger = 0;
   if (const char* sg = std::getenv("CET_STAGGER")) b.stagger = std::atoi(sg);
   b.enc_split = 0;
@@ -1473,8 +1483,12 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   // encoder split (v4): the encoders of a stack are independent until the decoder, so at small batches
   // each runs on its own workgroup (bf16 policy, no ProbSparse draws, production outputs only, the
   // whole grid resident at two workgroups per CU)
+  static const int64_t split_max = [] {   // CET_SPLIT_MAX: the largest B · n_enc split (A/B knob; default 512)
+    const char* v = std::getenv("CET_SPLIT_MAX");
+    return v ? (int64_t)std::atoll(v) : (int64_t)512;
+  }();
   const bool split = e->enc_split_ok && e->prec == 0 && p.n_enc > 1 && p.n_calls == 0 && !diag &&
-                     (int64_t)a.B * p.n_enc <= 512;
+                     (int64_t)a.B * p.n_enc <= split_max;
   if (split) {
     const size_t words = (size_t)a.B * p.S * (v4_rs(0) / 8);
     if (words > e->enc_xchg_n) {
@@ -1497,10 +1511,11 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   {
     // the instance launch_v4 takes (v4_instance: one decision for both sides)
     const int inst = v4_instance(b, e->prec, e->icfg.d_ff);
+    const int sh = inst == V4I_SHAPE || inst == V4I_SHAPE_STAMPS || (inst == V4I_SPLIT && b.shape == V4S_E43) ? b.shape : 0;
     char nm[160];
-    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %s, %s>", e->icfg.d_ff,
-                  inst == V4I_DIAG ? "true" : "false", e->prec, inst == V4I_SPLIT ? "true" : "false",
-                  inst == V4I_C2 || inst == V4I_C2_STAMPS ? "true" : "false", inst == V4I_C2_STAMPS ? "true" : "false");
+    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %d, %s>", e->icfg.d_ff,
+                  inst == V4I_DIAG ? "true" : "false", e->prec, inst == V4I_SPLIT ? "true" : "false", sh,
+                  inst == V4I_SHAPE_STAMPS ? "true" : "false");
     e->last_kernel = inst == V4I_NONE ? std::string() : std::string(nm);
   }
   return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);

@@ -17,9 +17,11 @@ namespace v4 {
 
 // P: precision of the dense (LSQ-quantisable) layers; DIAG: the instance that honours the optional
 // outputs (attns maps, activation dumps, phase stamps) — the production instance compiles them out.
+// SH: the plan's encoder rows as compile-time constants (cet_kernels.h v4_shape: 0 generic, 1 C2 — one encoder
+// 90 → 45 → 23 → 12 —, 2 the TimingAnalysis stack e_layers [4, 3] with a ≤ 16-row decoder over its 24 stack rows).
 // ST: a production instance that honours the phase stamps only (the C2 + stamps diagnostic build,
 // -DCET_C2_STAMPS: per-phase cycles of the instance the bench times).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false, bool ST = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false>
 __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(plan))
@@ -91,7 +93,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   // first attention phase (104.4 vs 105.4 us kernel alone; staging calls 1-2's tables the same way during
   // the first layer's FFN / distil phases measured slower: DESIGN §3.0e).
 #ifndef CET_NO_TAB_PRE
-  constexpr bool PRE = C2;
+  constexpr bool PRE = SH != V4S_GENERIC;
 #else
   constexpr bool PRE = false;
 #endif
@@ -147,7 +149,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   }
   auto pre_table = [&](int l) -> const uint8_t* {   // the pre-staged table of encoder layer l's call, or null
     if constexpr (!PRE) return nullptr;
-    return l == 0 && t0n ? CNT : nullptr;
+    return l == 0 && t0n ? CNT : nullptr;   // (encoder 0 only: enc_layer passes l = -1 for the others)
   };
 
   Res<MT> X;
@@ -223,13 +225,38 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     constexpr bool NKX_ = decltype(NKXc)::value;
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
+#if defined(CET_AB8) || defined(CET_AB8_ENC) || defined(CET_AB8_DEC) || defined(CET_AB8_NQ)
+    // the round-4 ab8 candidate: the head's K/V weights requested before the call's table setup (all
+    // calls, or only the encoder's (causal 0) / the decoder's (causal 1) self-attention calls)
+#if defined(CET_AB8)
+    const bool early = true;
+#elif defined(CET_AB8_ENC)
+    const bool early = !causal;
+#elif defined(CET_AB8_NQ)
+    const bool early = !causal && MQ_ == CET_AB8_NQ;
+#else
+    const bool early = causal;
+#endif
+    if (early) {
+      const KVPre<P> kvp = prefetch_kv<P>(io, M, w);
+      call_setup(io, call, pre);
+      attention_head<P, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
+    } else {
+      call_setup(io, call, pre);
+      attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
+    }
+#else
     call_setup(io, call, pre);
     attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
+#endif
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
     if (SPLIT && e != my_e) continue;   // the entry staging of x_enc is still intact for it
-    if (!SPLIT && e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);   // CTX was reused by encoder e-1
+    // CTX was reused by encoder e-1: re-stage x_enc (the window's embedding is recomputed over the whole
+    // sequence's circular conv: embed.py runs once in the reference, model.py:257-258, encoder.py:95-106;
+    // staging it under encoder 0's norm phase or with one f32x4 per thread measured no faster)
+    if (!SPLIT && e > 0) stage(a.x_enc + (size_t)b * L0 * C, IN, L0, C, CS);
     // ---- DataEmbedding (embed.py:132-135) on the EncoderStack window x[:, -L:] (encoder.py:95-106)
     int L = L0 >> e;
     const int off = L0 - L;
@@ -291,7 +318,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
           attend(NQ, NQ, std::true_type{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4, part_of(q, 0),
                  part_of(q, 128), part_of(q, 256), L, L, PL.prob, 0, 0, ELD.call,
                  DIAG && a.attns ? a.attns + ELD.attn_off + (size_t)b * ELD.attn_stride : nullptr,
-                 pre_table(l));
+                 pre_table(SH == V4S_C2 || e == 0 ? l : -1));   // C2: one encoder
         };
         switch (nmt) {
           case 1: enc_attend(IC<1>{}); break;
@@ -365,12 +392,25 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       (void)last_of_stack;
       return Lout;
     };
-    if constexpr (C2) {
-      // C2 (BASELINE configs[1]): one encoder of four layers, rows 90 → 45 → 23 → 12 (launch_v4 checks the plan)
+    if constexpr (SH == V4S_C2) {
+      // C2 (BASELINE configs[1]): one encoder of four layers, rows 90 → 45 → 23 → 12 (the host checks the plan)
       enc_layer(IC<90>{}, 0);
       enc_layer(IC<45>{}, 1);
       enc_layer(IC<23>{}, 2);
       L = enc_layer(IC<12>{}, 3);
+    } else if constexpr (SH == V4S_E43) {
+      // the TimingAnalysis stack (TimingAnalysis/config.py e_layers [4, 3]): encoder 0 as C2's, encoder 1 on the
+      // window x[:, -45:], rows 45 → 23 → 12
+      if (e == 0) {
+        enc_layer(IC<90>{}, 0);
+        enc_layer(IC<45>{}, 1);
+        enc_layer(IC<23>{}, 2);
+        L = enc_layer(IC<12>{}, 3);
+      } else {
+        enc_layer(IC<45>{}, 0);
+        enc_layer(IC<23>{}, 1);
+        L = enc_layer(IC<12>{}, 2);
+      }
     } else {
       for (int l = 0; l < PL.enc_layers[e]; ++l) L = enc_layer(ELD.L_in, l);
     }
@@ -426,6 +466,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   }
   auto decoder = [&](auto NMDc, auto NMSc) __attribute__((always_inline)) {
     constexpr int NMS = decltype(NMSc)::value;
+    // the cross-attention's key-tile bound is exact for one tile (S ≤ 16) and in the E43 instance (S = 24)
+    constexpr bool CROSS_EXACT = NMS == 1 || SH == V4S_E43;
     constexpr int NMD = decltype(NMDc)::value;
     const int nmd = NMD;
     Res<NMD> XD;
@@ -481,7 +523,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       {
         // cross-attention: FullAttention over the encoder-stack output, mix=False
 #ifndef CET_NO_CROSS_HOIST
-        attention_head<P, NMD, NMS, true, NMS == 1>(cio, M, w, CK, CV, cqp);
+        attention_head<P, NMD, NMS, true, CROSS_EXACT>(cio, M, w, CK, CV, cqp);
 #else
         const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
         // the key-tile bound MT is exact only for S in 81-96; NMS == 1 is exact (S ≤ 16)
@@ -561,7 +603,9 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     STAMP();  // final norm + projection
     if (stamps && threadIdx.x == 0) stamps[99] = __builtin_amdgcn_s_memrealtime();
   };
-  switch ((Ld + 15) >> 4) {
+  if constexpr (SH == V4S_E43) {
+    decoder(IC<1>{}, IC<2>{});   // the host checks dec_len ≤ 16 and S = 24
+  } else switch ((Ld + 15) >> 4) {
     case 1: S <= 16 ? decoder(IC<1>{}, IC<1>{}) : decoder(IC<1>{}, IC<MT>{}); break;
     case 2: S <= 16 ? decoder(IC<2>{}, IC<1>{}) : decoder(IC<2>{}, IC<MT>{}); break;
     default: S <= 16 ? decoder(IC<3>{}, IC<1>{}) : decoder(IC<3>{}, IC<MT>{}); break;
@@ -651,10 +695,10 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 }
 
 // X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, bool C2 = false, bool ST = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false>
 __global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
     informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
-  informer_forward_v4_body<DFF, DIAG, P, SPLIT, C2, ST>(a, plan);
+  informer_forward_v4_body<DFF, DIAG, P, SPLIT, SH, ST>(a, plan);
 }
 
 template <int P>
@@ -665,15 +709,26 @@ int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream)
   const bool split = a->enc_split != 0;
   switch (v4_instance(*a, P, dff)) {
     case V4I_SPLIT:   // encoder split: bf16 policy, production instance only (the launcher checks the plan)
-      if constexpr (P == P_BF16) kern = dff == 64 ? informer_forward_v4<64, false, P, true> : informer_forward_v4<128, false, P, true>;
+      if constexpr (P == P_BF16) {
+        if (a->shape == V4S_E43) kern = informer_forward_v4<64, false, P, true, V4S_E43>;
+        else kern = dff == 64 ? informer_forward_v4<64, false, P, true> : informer_forward_v4<128, false, P, true>;
+      }
       break;
 #ifdef CET_C2_STAMPS
-    case V4I_C2_STAMPS:   // C2 instance + phase stamps (diagnostic build)
-      if constexpr (P == P_BF16) kern = informer_forward_v4<64, false, P, false, true, true>;
+    case V4I_SHAPE_STAMPS:   // the shape instance + phase stamps (diagnostic build)
+      if constexpr (P == P_BF16) {
+        kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43, true>
+                                   : informer_forward_v4<64, false, P, false, V4S_C2, true>;
+      }
       break;
 #endif
-    case V4I_C2:
-      if constexpr (P != P_X3) kern = informer_forward_v4<64, false, P, false, true>;
+    case V4I_SHAPE:   // the plan's rows at compile time
+      if constexpr (P == P_BF16) {
+        kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43>
+                                   : informer_forward_v4<64, false, P, false, V4S_C2>;
+      } else if constexpr (P == P_FP8) {
+        kern = informer_forward_v4<64, false, P, false, V4S_C2>;
+      }
       break;
     case V4I_DIAG: kern = dff == 64 ? informer_forward_v4<64, true, P> : informer_forward_v4<128, true, P>; break;
     case V4I_GENERIC: kern = dff == 64 ? informer_forward_v4<64, false, P> : informer_forward_v4<128, false, P>; break;

@@ -40,21 +40,27 @@ struct InformerArgs {
   unsigned* enc_count;        // [B] arrivals (the last arrival re-arms it)
   int stagger;                // experiment (CET_STAGGER=mask:units): workgroups with (b & mask) != 0 sleep units·64
                               // cycles at entry (-DCET_STAGGER builds only)
-  int c2;                     // the plan is C2's encoder (one encoder, rows 90 → 45 → 23 → 12): the
-                              // bf16 production launch takes the instance with those rows at compile time
+  int shape;                  // v4_shape of the plan (V4S_*): the bf16 production launch takes the instance with its
+                              // encoder rows as compile-time constants
 };
+
+// Plans with a compile-time instance (cet_api.cpp plan_shape): C2's encoder (one encoder, rows 90 → 45 → 23 → 12,
+// the first three distilling) and the TimingAnalysis stack (e_layers [4, 3]: that encoder plus one on the window
+// x[:, -45:], rows 45 → 23 → 12; 24 stack rows, a decoder of at most 16 rows).
+enum V4Shape { V4S_GENERIC = 0, V4S_C2 = 1, V4S_E43 = 2 };
 
 // The v4 Informer instance a launch takes.  launch_v4 (cet_informer4.hpp) launches exactly this choice and
 // the host reports it (cet_last_kernel), so the two agree by construction.  prec: 0 bf16, 1 split bf16, 2 fp8.
-enum V4Instance { V4I_NONE = 0, V4I_GENERIC = 1, V4I_DIAG = 2, V4I_C2 = 3, V4I_SPLIT = 4, V4I_C2_STAMPS = 5 };
+enum V4Instance { V4I_NONE = 0, V4I_GENERIC = 1, V4I_DIAG = 2, V4I_SHAPE = 3, V4I_SPLIT = 4, V4I_SHAPE_STAMPS = 5 };
 __host__ __device__ inline int v4_instance(const InformerArgs& a, int prec, int dff) {
   const bool diag = a.attns || a.dbg || a.stamps;
   if (dff != 64 && dff != 128) return V4I_NONE;
-  if (a.enc_split) return prec == 0 && !diag ? V4I_SPLIT : V4I_NONE;   // bf16 production only
+  if (a.enc_split) return prec == 0 && !diag && (a.shape != V4S_E43 || dff == 64) ? V4I_SPLIT : V4I_NONE;
 #ifdef CET_C2_STAMPS
-  if (dff == 64 && a.c2 && a.stamps && !a.attns && !a.dbg && prec == 0) return V4I_C2_STAMPS;
+  if (dff == 64 && a.shape != V4S_GENERIC && a.stamps && !a.attns && !a.dbg && prec == 0) return V4I_SHAPE_STAMPS;
 #endif
-  if (dff == 64 && a.c2 && !diag && prec != 1) return V4I_C2;   // the C2 plan's compile-time row counts
+  // compile-time rows: C2 for bf16 and fp8, E43 for bf16
+  if (dff == 64 && !diag && ((a.shape == V4S_C2 && prec != 1) || (a.shape == V4S_E43 && prec == 0))) return V4I_SHAPE;
   return diag ? V4I_DIAG : V4I_GENERIC;
 }
 

@@ -57,6 +57,11 @@ struct Geo {
   static constexpr int IMG = LMAX * RS;                // one plane of a LMAX-row image
 };
 
+#ifdef CET_AB8_DUMP
+// diagnostic (round-5 investigation of the ab8 candidate): head 0 of workgroup 0's first 6-tile attention call
+// writes its K/V tiles, the first selected tile's softmax statistics and context to this array
+__device__ unsigned int g_ab8_dump[8][128 * 64];   // per head
+#endif
 // ------------------------------------------------------------------ fragments and products
 template <int P>
 struct XF {  // B-role (activation) fragment of one 16x16x32 k-step
@@ -916,7 +921,8 @@ template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false, bool NKX = false
 __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
                                                const AF<plain_of<PD>()>* kin = nullptr,
                                                const AF<plain_of<PD>()>* vin = nullptr,
-                                               const WPre<PD, 4>* qpre = nullptr) {
+                                               const WPre<PD, 4>* qpre = nullptr,
+                                               const KVPre<PD>* kvpre = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -953,10 +959,33 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       Kf[mt] = kin[mt];
       Vf[mt] = vin[mt];
     }
+  } else if (kvpre) {
+    project_kv<PD, MK>(io, *kvpre, Kf, Vf);   // weights requested by the caller (CET_AB8 experiment)
   } else {
     project_kv<PD, MK>(io, m, h, Kf, Vf);
   }
   SUB(1);
+#ifdef CET_AB8_DUMP
+  if constexpr (MQ == 6 && !EXTKV) {
+    if (blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u) {
+#pragma unroll
+      for (int t = 0; t < MK; ++t) {
+        const uint2 kh = __builtin_bit_cast(uint2, Kf[t].h), vh = __builtin_bit_cast(uint2, Vf[t].h);
+        g_ab8_dump[h][(4 * t + 0) * 64 + lane] = kh.x;
+        g_ab8_dump[h][(4 * t + 1) * 64 + lane] = kh.y;
+        g_ab8_dump[h][(4 * t + 2) * 64 + lane] = vh.x;
+        g_ab8_dump[h][(4 * t + 3) * 64 + lane] = vh.y;
+        if constexpr (PA == P_X3) {
+          const uint2 kl = __builtin_bit_cast(uint2, Kf[t].l), vl = __builtin_bit_cast(uint2, Vf[t].l);
+          g_ab8_dump[h][(24 + 4 * t + 0) * 64 + lane] = kl.x;
+          g_ab8_dump[h][(24 + 4 * t + 1) * 64 + lane] = kl.y;
+          g_ab8_dump[h][(24 + 4 * t + 2) * 64 + lane] = vl.x;
+          g_ab8_dump[h][(24 + 4 * t + 3) * 64 + lane] = vl.y;
+        }
+      }
+    }
+  }
+#endif
   // Q tiles are projected where they are consumed (per query tile in M, per selected tile in the
   // softmax): wq and its epilogue vectors are the only Q state that lives
   if constexpr (!EARLYQ) {
@@ -1153,6 +1182,33 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
     sum = xor_sum(sum, 16);
     sum = xor_sum(sum, 32);
     const float inv = __builtin_amdgcn_rcpf(sum);
+#ifdef CET_AB8_DUMP
+    if constexpr (MQ == 6 && !EXTKV) {
+      if (blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u) {
+        g_ab8_dump[h][(64 + 8 * st + 0) * 64 + lane] = __float_as_uint(mx);
+        g_ab8_dump[h][(64 + 8 * st + 1) * 64 + lane] = __float_as_uint(sum);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g_ab8_dump[h][(64 + 8 * st + 2 + r) * 64 + lane] = __float_as_uint(o[r]);
+        g_ab8_dump[h][(64 + 8 * st + 6) * 64 + lane] = (unsigned)qi;
+      }
+      if (blockIdx.x == 0 && st == 0 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u) {
+        const uint2 qh = __builtin_bit_cast(uint2, qs.h);
+        g_ab8_dump[h][48 * 64 + lane] = qh.x;
+        g_ab8_dump[h][49 * 64 + lane] = qh.y;
+        g_ab8_dump[h][50 * 64 + lane] = __float_as_uint(mx);
+        g_ab8_dump[h][51 * 64 + lane] = __float_as_uint(sum);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g_ab8_dump[h][(52 + r) * 64 + lane] = __float_as_uint(o[r]);
+        if constexpr (PA == P_X3) {
+          const uint2 ql = __builtin_bit_cast(uint2, qs.l);
+          g_ab8_dump[h][56 * 64 + lane] = ql.x;
+          g_ab8_dump[h][57 * 64 + lane] = ql.y;
+        }
+      }
+      if (blockIdx.x == 0 && st == nst - 1 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u)
+        g_ab8_dump[h][127 * 64 + lane] = 1u;   // written once per launch sequence (the host clears it)
+    }
+#endif
     if (i < nsel) {
       ctx_st4(qi, g * 4, o * inv);
       if (io.attn_out) {

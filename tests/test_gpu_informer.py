@@ -394,6 +394,8 @@ def test_full_size_production_launch_vs_oracle(name, B):
     cfg = case.cfg
     xe, xd, _ = make_batch(B, cfg["seq_len"], cfg["label_len"], cfg["pred_len"], seed=500 + B)
     out, _, _ = run_engine(m, xe, xd, case.idx)
+    if name.endswith("_e43"):   # the e_layers [4, 3] stack takes its compile-time instance (plan_shape)
+        assert m.engine(torch.device("cuda:0")).last_kernel() == E43_KERNEL
     rows = np.r_[0:32, B - 32:B]
     ref, _ = oracle_for(case).forward(xe[rows], xd[rows], case.idx)
     assert np.isfinite(out).all()
@@ -416,6 +418,7 @@ def test_encoder_split_small_batches_vs_oracle(B):
     cfg = case.cfg
     xe, xd, _ = make_batch(B, cfg["seq_len"], cfg["label_len"], cfg["pred_len"], seed=900 + B)
     out, _, _ = run_engine(m, xe, xd, case.idx)
+    assert m.engine(torch.device("cuda:0")).last_kernel() == E43_SPLIT_KERNEL
     again, _, _ = run_engine(m, xe, xd, case.idx)
     np.testing.assert_array_equal(out, again)
     rows = np.arange(B) if B <= 64 else np.r_[0:32, B - 32:B]
@@ -709,7 +712,9 @@ def test_fused_nmse_odd_batch_and_label_width(c_out):
     np.testing.assert_allclose((s[0] / s[1]).cpu().numpy(), ref_split(o.cpu().numpy(), lab_np), rtol=1e-5)
 
 
-C2_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, true, false>"
+C2_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, 1, false>"     # plan_shape V4S_C2
+E43_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, 2, false>"    # V4S_E43 (TimingAnalysis stack)
+E43_SPLIT_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, true, 2, false>"
 
 
 def _c2_model(attn, seed, bias_offset=0.0):

@@ -19,17 +19,36 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from channelestimationtransformer_amd.dataset import make_batch  # noqa: E402
 
-NAMES = (["start", "embedding"] + sum([[f"L{l} attention", f"L{l} O-proj+LN1", f"L{l} FFN+LN2"] +
-                                       ([f"L{l} conv+pool"] if l < 3 else []) for l in range(4)], []) +
-         ["enc norm", "dec embedding"] +
-         sum([[f"D{l} self-attn", f"D{l} cross-attn", f"D{l} O/LN/FFN rest"] for l in range(3)], []) +
-         ["final norm+proj"])
+def names(e_layers=(4,), d_layers=3):
+    """Phase names in STAMP order: per encoder its embedding, layers (attention, O-proj + LN1, FFN + LN2, distil
+    conv on all but the last) and norm; then the decoder."""
+    n = ["start"]
+    for e, nl in enumerate(e_layers):
+        p = f"E{e} " if len(e_layers) > 1 else ""
+        n += [f"{p}embedding"]
+        n += sum([[f"{p}L{l} attention", f"{p}L{l} O-proj+LN1", f"{p}L{l} FFN+LN2"] +
+                  ([f"{p}L{l} conv+pool"] if l < nl - 1 else []) for l in range(nl)], [])
+        n += [f"{p}enc norm"]
+    n += ["dec embedding"] + sum([[f"D{l} self-attn", f"D{l} cross-attn", f"D{l} O/LN/FFN rest"]
+                                  for l in range(d_layers)], []) + ["final norm+proj"]
+    return n
+
+
+NAMES = names()
 
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    e43 = len(sys.argv) > 2 and sys.argv[2] == "e43"   # the TimingAnalysis stack (attn full, e_layers [4, 3])
     dev = torch.device("cuda:0")
-    m = bench.build_model(dev)
+    if e43:
+        from channelestimationtransformer_amd.latency import CONFIG, build
+
+        m = build(dict(CONFIG), dev)
+        global NAMES
+        NAMES = names((4, 3))
+    else:
+        m = bench.build_model(dev)
     eng = m.engine(dev)
     eng.seed(1)
     xe, xd, _ = make_batch(B, seed=5)
