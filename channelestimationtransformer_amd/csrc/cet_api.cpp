@@ -760,7 +760,7 @@ int build_informer(cet_engine* e) {
     ac.LK = e->calls[k].LK;
     ac.U = e->calls[k].U;
     ac.u = u_part(c.factor, ac.LQ);
-    ac.cnt_stride = 6 * 16;   // fixed 96-byte rows: every key tile of a query row is in bounds
+    ac.cnt_stride = CNT_STRIDE;   // fixed rows (cet_plan.hpp): every key tile of a query row is in bounds
     ac.cnt_off = coff;
     coff += (uint32_t)(r16(ac.LQ) * ac.cnt_stride);
     coff = (coff + 15) & ~15u;
@@ -786,7 +786,7 @@ int build_informer(cet_engine* e) {
   int max_cnt = 0;
   for (int k = 0; k < p.n_calls; ++k)
     if (p.calls[k].u < p.calls[k].LQ) max_cnt = std::max(max_cnt, r16(p.calls[k].LQ) * p.calls[k].cnt_stride);
-  if (max_cnt > LMAX * 96 || LP > LMAX || (c.enc_in & 3))
+  if (max_cnt > LMAX * CNT_STRIDE || LP > LMAX || (c.enc_in & 3))
     return fail(CET_E_INVALID, "fused LDS layout: multiplicity table or sequence length out of range");
   // v4: fixed regions (cet_plan.hpp v4_*) | stack output | [x_dec staged at entry, when two sequences
   // per CU still fit with it: its HBM latency then overlaps the LDS zeroing; else it is requested
@@ -839,7 +839,10 @@ int build_lw(cet_engine* e) {
   m->act = c.act_relu ? 2 : 1;
   m->stack = c.stack;
   m->out_attn = c.output_attention;
-  e->prec = 3;
+  // "bf16" on a layer-wise engine: bf16 GEMM operands in the fused form (cet_lwf.hip); "auto" stays fp32, the
+  // reference's arithmetic class for these shapes
+  m->bf16 = e->prec_req == 0;
+  e->prec = m->bf16 ? 0 : 3;
   auto Wq = [&](const std::string& n) {   // a quantisable module's weight, LSQ applied
     std::vector<float> w = e->W(n + ".weight");
     if (lsq && e->has(n + ".step_size")) {
@@ -1565,9 +1568,14 @@ static int forward_lw(cet_engine* e, const float* x_enc, const float* x_dec, int
   }
   const int tk = timing_mark(e, st);
   const int rc = e->lw->forward(x_enc, x_dec, B, out, attns, e->lw->d_idx, st);
+  if (rc == -7)
+    return fail(CET_E_INVALID, "bf16 operands need the fused layer-wise form (no attention maps, a working set that "
+                               "fits one workgroup, feature counts that are multiples of 8)");
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   e->last_path = e->lw->last_fused ? CET_PATH_LW_FUSED : CET_PATH_LW;
-  e->last_kernel = e->lw->last_fused ? "cet::lw::lw_fused" : "";   // the operator path launches several kernels
+  e->last_kernel = !e->lw->last_fused ? ""   // the operator path launches several kernels
+                  : e->lw->bf16        ? "cet::lw::lw_fused (bf16 operands)"
+                                       : "cet::lw::lw_fused";
   if (rc) return fail(CET_E_HIP, std::string("layer-wise launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (label && cet_launch_nmse_split(out, label, B, e->icfg.out_len, e->icfg.c_out, nmse_acc, nullptr, 1, nmse_sums, st))
     return fail(CET_E_HIP, "nmse launch failed");
@@ -1691,7 +1699,7 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     const bool prep = B >= cet_engine::PREP_MIN_B;
     if (prep && !e->tab_ready) {
       // first forward after a (re)seed: this forward's tables from a one-workgroup launch
-      const int lds = std::max(640 * 4 + LMAX * 96, std::min(replay_fast_lds(p), 64 * 1024));
+      const int lds = std::max(640 * 4 + LMAX * CNT_STRIDE, std::min(replay_fast_lds(p), 64 * 1024));
       if (cet_launch_sampler_prep((const InformerPlan*)e->d_plan, e->d_mt + 640 * e->mt_cur,
                                   e->d_mt + 640 * (1 - e->mt_cur), e->d_tab[e->tab_cur], lds, st))
         return fail(CET_E_HIP, std::string("sampler prep launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -1778,8 +1786,9 @@ int cet_set_precision(cet_engine* e, int prec) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   if (e->kind != 0) return fail(CET_E_INVALID, "precision modes are Informer-engine only");
   if (prec < -1 || prec > 2) return fail(CET_E_INVALID, "precision must be -1 (auto), 0 (bf16), 1 (split bf16) or 2 (fp8)");
-  if (e->generic && prec != -1)
-    return fail(CET_E_INVALID, "the layer-wise engine (shapes outside the fused kernels) computes in fp32 only");
+  if (e->generic && prec != -1 && prec != 0)
+    return fail(CET_E_INVALID, "the layer-wise engine (shapes outside the fused kernels) computes in fp32, or in bf16 "
+                               "operands in its fused form");
   e->prec_req = prec;
   e->dirty = true;
   return CET_OK;

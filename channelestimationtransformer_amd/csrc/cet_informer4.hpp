@@ -225,30 +225,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     constexpr bool NKX_ = decltype(NKXc)::value;
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
-#if defined(CET_AB8) || defined(CET_AB8_ENC) || defined(CET_AB8_DEC) || defined(CET_AB8_NQ)
-    // the round-4 ab8 candidate: the head's K/V weights requested before the call's table setup (all
-    // calls, or only the encoder's (causal 0) / the decoder's (causal 1) self-attention calls)
-#if defined(CET_AB8)
-    const bool early = true;
-#elif defined(CET_AB8_ENC)
-    const bool early = !causal;
-#elif defined(CET_AB8_NQ)
-    const bool early = !causal && MQ_ == CET_AB8_NQ;
-#else
-    const bool early = causal;
-#endif
-    if (early) {
-      const KVPre<P> kvp = prefetch_kv<P>(io, M, w);
-      call_setup(io, call, pre);
-      attention_head<P, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
-    } else {
-      call_setup(io, call, pre);
-      attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
-    }
-#else
     call_setup(io, call, pre);
     attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
-#endif
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
@@ -417,7 +395,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     nmt = (L + 15) >> 4;
     // ---- Encoder.norm (encoder.py:83-84) → this encoder's rows of the stack output (ENC)
     const int rows = PL.enc_rows[e];
-    const Img<P> encw{ENC.base + PL.enc_row_off[e] * G::RS, ENC.lo};
+    const ImgRows<P> encw{ENC, PL.enc_row_off[e]};
     ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, XB, &encw);
     __syncthreads();
     if (dbg && PL.enc_dbg[e] >= 0) dump_res(X, nmt, rows, dbg + PL.enc_dbg[e]);

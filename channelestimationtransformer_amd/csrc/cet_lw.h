@@ -86,6 +86,7 @@ constexpr int F_MAX_ENC = 4, F_MAX_EL = 8, F_MAX_DEC = 4, F_MAX_CALLS = F_MAX_EN
 constexpr int F_LMAX = 128;   // rows per sequence (8 m-tiles)
 struct FG {
   uint32_t w;      // packed weight (float offset into the packed blob)
+  uint32_t wb;     // the same weight as bf16 fragments (16-byte offset into the bf16 blob; the bf16 instance)
   uint32_t b, s;   // bias / scale (float offsets into the model blob) or FNONE
   int N, K;
 };
@@ -115,9 +116,11 @@ struct FPlan {
   FDec dec[F_MAX_DEC];
 };
 bool plan_is_d64(const FPlan& p);   // the plan equals the compile-time d_model-64 layout (cet_lwf.hip D64Plan)
-int launch_fused(const FPlan* d_plan, int D, bool fix, size_t lds_bytes, const float* blob, const float* pw, const float* x_enc,
-                 const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st);
-int prepare_fused(int D, bool fix);
+// bf: GEMM operands in bf16 (v_mfma_f32_16x16x32_bf16, weights from pwb) instead of fp32
+int launch_fused(const FPlan* d_plan, int D, bool fix, bool bf, size_t lds_bytes, const float* blob, const float* pw,
+                 const void* pwb, const float* x_enc, const float* x_dec, float* out, const int32_t* idx, int B,
+                 hipStream_t st);
+int prepare_fused(int D, bool fix, bool bf);
 
 // ------------------------------------------------------------------ host model (cet_lw_host.cpp)
 // Weights as fp32 [N][K] matrices in one device blob (float offsets below); ProbSparse draws of a
@@ -174,9 +177,14 @@ struct Model {
   bool fused_ok = false, use_fused = true, last_fused = false;
   size_t fused_lds = 0;
   bool fused_fix = false;   // the plan is the compile-time d_model-64 layout (launch_fused's FIX instance)
+  // bf16 GEMM operands (cet_set_precision "bf16" on a layer-wise engine): the fused form only, for feature
+  // counts that are multiples of 8 (a lane's 8 consecutive k never straddle a conv tap)
+  bool bf16 = false, fused_bf_ok = false;
   std::vector<float> pblob;
+  std::vector<uint16_t> pbblob;   // Wb[nt][ks][lane][j] = bf16(W[16nt + (lane & 15)][32ks + 8(lane >> 4) + j])
   FPlan* d_fplan = nullptr;
   float* d_pblob = nullptr;
+  uint16_t* d_pbblob = nullptr;
   int build_fused();
   ~Model();
   size_t ws_floats(int B) const;

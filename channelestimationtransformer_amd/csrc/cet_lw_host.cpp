@@ -13,6 +13,13 @@
 namespace cet {
 namespace lw {
 
+static uint16_t bf16_rne(float f) {   // fp32 → bf16, round to nearest even (finite weights)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
 Model::~Model() {
   if (gexec) (void)hipGraphExecDestroy(gexec);
   if (dexec) (void)hipGraphExecDestroy(dexec);
@@ -22,6 +29,7 @@ Model::~Model() {
   if (d_idx) (void)hipFree(d_idx);
   if (d_fplan) (void)hipFree(d_fplan);
   if (d_pblob) (void)hipFree(d_pblob);
+  if (d_pbblob) (void)hipFree(d_pbblob);
 }
 
 size_t Model::push(const std::vector<float>& v) {
@@ -103,8 +111,10 @@ int Model::build_fused() {
   fused_lds = o * sizeof(float);
   if (why) fprintf(stderr, "lw fused: lds %zu bytes, attention on %d waves\n", fused_lds, p.attn_waves);
   if (fused_lds > 160 * 1024) return 0;
-  // packed weights: Wp[nt][kq][lane][j] = W[16nt + (lane & 15)][16kq + 4j + (lane >> 4)]
+  // packed weights: Wp[nt][kq][lane][j] = W[16nt + (lane & 15)][16kq + 4j + (lane >> 4)], and for the bf16
+  // instance Wb[nt][ks][lane][j] = bf16(W[16nt + (lane & 15)][32ks + 8(lane >> 4) + j]) (round to nearest even)
   pblob.clear();
+  pbblob.clear();
   auto pack = [&](size_t w, int N, int K, size_t bias, size_t scale) {
     const int NT = (N + 15) / 16, KQ = (K + 15) / 16;
     const size_t at = pblob.size();
@@ -116,8 +126,18 @@ int Model::build_fused() {
             const int n = 16 * nt + (lane & 15), k = 16 * kq + 4 * j + (lane >> 4);
             if (n < N && k < K) pblob[at + (((size_t)nt * KQ + kq) * 64 + lane) * 4 + j] = blob[w + (size_t)n * K + k];
           }
+    const int KS = (K + 31) / 32;
+    const size_t atb = pbblob.size();
+    pbblob.resize(atb + (size_t)NT * KS * 512, 0);
+    for (int nt = 0; nt < NT; ++nt)
+      for (int ks = 0; ks < KS; ++ks)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + j;
+            if (n < N && k < K) pbblob[atb + (((size_t)nt * KS + ks) * 64 + lane) * 8 + j] = bf16_rne(blob[w + (size_t)n * K + k]);
+          }
     FG g;
-    g.w = (uint32_t)at; g.b = (uint32_t)bias; g.s = scale == (size_t)-1 ? FNONE : (uint32_t)scale; g.N = N; g.K = K;
+    g.w = (uint32_t)at; g.wb = (uint32_t)(atb / 8); g.b = (uint32_t)bias; g.s = scale == (size_t)-1 ? FNONE : (uint32_t)scale; g.N = N; g.K = K;
     return g;
   };
   const size_t none = (size_t)-1;
@@ -156,17 +176,22 @@ int Model::build_fused() {
   for (size_t c = 0; c < call_u.size(); ++c) {
     p.call_U[c] = call_U[c]; p.call_u[c] = call_u[c]; p.call_off[c] = (uint32_t)idx_off[c];
   }
-  if (blob.size() >= FNONE || pblob.size() >= FNONE) return 0;
+  if (blob.size() >= FNONE || pblob.size() >= FNONE || pbblob.size() / 8 >= FNONE) return 0;
   if (!d_fplan && hipMalloc((void**)&d_fplan, sizeof(FPlan)) != hipSuccess) return -1;
   if (d_pblob) (void)hipFree(d_pblob);
   d_pblob = nullptr;
   if (hipMalloc((void**)&d_pblob, pblob.size() * sizeof(float)) != hipSuccess) return -1;
   if (hipMemcpy(d_pblob, pblob.data(), pblob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (d_pbblob) (void)hipFree(d_pbblob);
+  d_pbblob = nullptr;
+  if (hipMalloc((void**)&d_pbblob, pbblob.size() * sizeof(uint16_t)) != hipSuccess) return -1;
+  if (hipMemcpy(d_pbblob, pbblob.data(), pbblob.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  fused_bf_ok = C % 8 == 0 && Cd % 8 == 0 && D % 8 == 0 && HE % 8 == 0 && dff % 8 == 0;
   if (hipMemcpy(d_fplan, &p, sizeof(FPlan), hipMemcpyHostToDevice) != hipSuccess) return -1;
   const char* fenv = std::getenv("CET_LW_FUSED_FIX");
   fused_fix = plan_is_d64(p) && !(fenv && std::strcmp(fenv, "0") == 0);
   if (why) fprintf(stderr, "lw fused: compile-time d64 layout %s\n", fused_fix ? "yes" : "no");
-  if (prepare_fused(D, fused_fix)) return -1;
+  if (prepare_fused(D, fused_fix, bf16 && fused_bf_ok)) return -1;
   fused_ok = true;
   return 0;
 }
@@ -220,7 +245,10 @@ int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, fl
                    hipStream_t st) {
   // the fused form: one launch, no workspace, no staging copies
   last_fused = fused_ok && use_fused && !(attns && out_attn);
-  if (last_fused) return launch_fused(d_fplan, D, fused_fix, fused_lds, d_blob, d_pblob, x_enc, x_dec, out, idx_dev, B, st);
+  if (bf16 && !(last_fused && fused_bf_ok)) return -7;   // bf16 operands exist in the fused form only
+  if (last_fused)
+    return launch_fused(d_fplan, D, fused_fix, bf16, fused_lds, d_blob, d_pblob, d_pbblob, x_enc, x_dec, out, idx_dev,
+                        B, st);
   if (ensure_ws(B)) return -1;
   if (attns && out_attn) return enqueue(x_enc, x_dec, B, out, attns, idx_dev, st);
   const Key key{x_enc, x_dec, out, idx_dev, B};

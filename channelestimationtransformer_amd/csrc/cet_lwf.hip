@@ -78,8 +78,9 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in HBM instead of Y.  MT is compile-time, so the K loop is
 // straight-line code (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A
 // reads of k ≥ K land in the padded, finite part of the LDS image and meet zero weights.
-template <int AMODE, int MT, int NF = 0, int KF = 0>
-__device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw, const FG g,
+template <bool BF, int AMODE, int MT, int NF = 0, int KF = 0>
+__device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw,
+                                        const bf16x8* __restrict__ pwb, const FG g,
                                         int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
                                         int act, int res, float* __restrict__ gout, int t0, int ldo, int m0, int n0,
                                         int nstep) {
@@ -104,6 +105,69 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
     } else {
       rowoff[m][0] = rowoff[m][1] = rowoff[m][2] = A + t * lda;
     }
+  }
+  auto store = [&](int m, int n, const f32x4& acc, float sc, float bi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = 16 * (m0 + m) + 4 * q4 + r;
+      if (t >= L) continue;
+      float y = acc[r] * sc + bi;
+      if (pe) y += pe[t * N + n];
+      y = act_of(y, act);
+      if (res) y += lsm[Y + t * ldy + n];
+      if (gout) {
+        if (t >= t0) gout[(t - t0) * ldo + n] = y;
+      } else {
+        lsm[Y + t * ldy + n] = y;
+      }
+    }
+  };
+  if constexpr (BF) {
+    // bf16 operands on v_mfma_f32_16x16x32_bf16: per 32-k step the lane's 8 consecutive k of its A row
+    // (converted in registers, round to nearest even) against one 16-byte weight fragment (host-packed,
+    // cet_lw.h pbblob); fp32 accumulation and epilogue as below.  The k of a lane never straddle a conv tap
+    // (feature counts are multiples of 8: fused_bf_ok); k ≥ K read the padded, finite LDS and meet zero
+    // weights.
+    // compile-time K: every fragment of the n-tile requested up front; runtime K: one per step
+    const int KS = (K + 31) >> 5;
+    constexpr int KSM = KF ? (KF + 31) / 32 : 8;   // K ≤ 256
+    constexpr int KSP = KF ? KSM : 1;
+    for (int nt = n0; nt < NT; nt += nstep) {
+      const int n = 16 * nt + r16;
+      const float sc = has_s && n < N ? blob[g.s + n] : 1.f;
+      const float bi = has_b && n < N ? blob[g.b + n] : 0.f;
+      const bf16x8* wp = pwb + g.wb + (size_t)nt * KS * 64 + lane;
+      bf16x8 wv[KSP];
+      if constexpr (KF) {
+#pragma unroll
+        for (int ks = 0; ks < KSM; ++ks) wv[ks] = wp[(size_t)ks * 64];
+      }
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSM; ++ks) {
+        if (ks < KS) {
+          const bf16x8 w8 = KF ? wv[KF ? ks : 0] : wp[(size_t)ks * 64];
+          const int k = 32 * ks + 8 * q4;
+          int tap = 0, c = k;
+          if (AMODE) {
+            tap = (k >= Cin) + (k >= 2 * Cin);
+            c = k - tap * Cin;
+          }
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const float* src = lsm + (AMODE ? (tap == 0 ? rowoff[m][0] : tap == 1 ? rowoff[m][1] : rowoff[m][2]) : rowoff[m][0]) + c;
+            const f32x4 lo = {src[0], src[1], src[2], src[3]}, hi = {src[4], src[5], src[6], src[7]};
+            acc[m] = mfma16x16x32(cvt8(lo, hi), w8, acc[m]);
+          }
+        }
+      }
+      if (n >= N) continue;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) store(m, n, acc[m], sc, bi);
+    }
+    return;
   }
   for (int nt = n0; nt < NT; nt += nstep) {
     const int n = 16 * nt + r16;
@@ -154,40 +218,26 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
     }
     if (n >= N) continue;
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = 16 * (m0 + m) + 4 * q4 + r;
-        if (t >= L) continue;
-        float y = acc[m][r] * sc + bi;
-        if (pe) y += pe[t * N + n];
-        y = act_of(y, act);
-        if (res) y += lsm[Y + t * ldy + n];
-        if (gout) {
-          if (t >= t0) gout[(t - t0) * ldo + n] = y;
-        } else {
-          lsm[Y + t * ldy + n] = y;
-        }
-      }
-    }
+    for (int m = 0; m < MT; ++m) store(m, n, acc[m], sc, bi);
   }
 }
 
 // The GEMM's task split over the eight waves (≤ 48 rows: the plan's validated range, cet_lw_host.cpp
 // build_fused): two m-tiles are split between the wave halves, one or three stay whole per wave.
-template <int AMODE, int NF = 0, int KF = 0>
-__device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw, const FG g, int A,
+template <bool BF, int AMODE, int NF = 0, int KF = 0>
+__device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw,
+                                      const bf16x8* __restrict__ pwb, const FG g, int A,
                                       int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe, int act,
                                       int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
   const int w = uni(threadIdx.x >> 6);
   A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
   switch ((L + 15) >> 4) {
-    case 1: fgemm_t<AMODE, 1, NF, KF>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    case 1: fgemm_t<BF, AMODE, 1, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
     case 2:
-      fgemm_t<AMODE, 1, NF, KF>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, w / (NW / 2), w % (NW / 2),
+      fgemm_t<BF, AMODE, 1, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, w / (NW / 2), w % (NW / 2),
                         NW / 2);
       break;
-    default: fgemm_t<AMODE, 3, NF, KF>(blob, pw, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    default: fgemm_t<BF, AMODE, 3, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
   }
 }
 
@@ -444,10 +494,11 @@ struct D64Plan {
 };
 
 // NC: LayerNorm chunks of 16 features per lane row (d_model ≤ 16·NC)
-template <int NC, bool FIX = false>
+// BF: bf16 GEMM operands (fgemm_t), weights from pwb
+template <int NC, bool FIX = false, bool BF = false>
 __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) lw_fused(
     const FPlan* __restrict__ p, const float* __restrict__ blob, const float* __restrict__ pw,
-    const float* __restrict__ x_enc, const float* __restrict__ x_dec, float* __restrict__ out,
+    const bf16x8* __restrict__ pwb, const float* __restrict__ x_enc, const float* __restrict__ x_dec, float* __restrict__ out,
     const int32_t* __restrict__ idx) {
 #define PV(f) (FIX ? D64Plan::f : p->f)
 #define PA(f, i) (FIX ? D64Plan::f[i] : p->f[i])
@@ -477,7 +528,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   LWF_ST(3)
   // ---- DataEmbedding of the encoder input, straight into encoder 0's rows; a stack keeps the rows of the
   //      later encoders' windows x[:, -L0/2:] (each later window is a suffix of it) in E1
-  fgemm<1, FIX ? 64 : 0, FIX ? 48 : 0>(blob, pw, p->emb_e, T, PV(ldIN), PV(C), L0, X, ldD, blob + p->pe_e, 0, 0);
+  fgemm<BF, 1, FIX ? 64 : 0, FIX ? 48 : 0>(blob, pw, pwb, p->emb_e, T, PV(ldIN), PV(C), L0, X, ldD, blob + p->pe_e, 0, 0);
   __syncthreads();
   LWF_ST(0)
   const int e1rows = PV(e1_rows);
@@ -495,7 +546,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     const int L = Lc;
     int Lout = L;
     const FEnc* ly = &p->enc[i][l];
-    fgemm<0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
+    fgemm<BF, 0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->qkv, X, ldD, 0, L, T, ldT, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
     {
@@ -507,17 +558,17 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     }
     __syncthreads();
     LWF_ST(1)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
     const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
     __syncthreads();
     LWF_ST(0)
     fln<NC>(X, ldD, L, D, n1, X, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
     __syncthreads();
     LWF_ST(0)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
     const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
     __syncthreads();
     LWF_ST(0)
@@ -525,7 +576,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     __syncthreads();
     LWF_ST(2)
     if (ly->conv) {   // ConvLayer: conv + BN(eval) folded + ELU, then MaxPool1d(3, 2, 1)
-      fgemm<1, FIX ? 64 : 0, FIX ? 192 : 0>(blob, pw, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
+      fgemm<BF, 1, FIX ? 64 : 0, FIX ? 192 : 0>(blob, pw, pwb, ly->cv, X, ldD, D, L, T, ldF, nullptr, 3, 0);
       __syncthreads();
       LWF_ST(0)
       const int Lo = ly->Lo;
@@ -591,7 +642,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   }
   __syncthreads();
   LWF_ST(3)
-  fgemm<1, FIX ? 64 : 0, FIX ? 48 : 0>(blob, pw, p->emb_d, T, PV(ldINd), PV(Cd), Ld, XD, ldD, blob + p->pe_d, 0, 0);
+  fgemm<BF, 1, FIX ? 64 : 0, FIX ? 48 : 0>(blob, pw, pwb, p->emb_d, T, PV(ldINd), PV(Cd), Ld, XD, ldD, blob + p->pe_d, 0, 0);
   __syncthreads();
   LWF_ST(0)
   const int S = PV(S);
@@ -599,7 +650,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   #pragma unroll 1
   for (int l = 0; l < PV(ndec); ++l) {
     const FDec* ly = &p->dec[l];
-    fgemm<0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, ly->qkv, XD, ldD, 0, Ld, T, ldT, nullptr, 0, 0);
+    fgemm<BF, 0, FIX ? 192 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->qkv, XD, ldD, 0, Ld, T, ldT, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
     {
@@ -611,31 +662,31 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     }
     __syncthreads();
     LWF_ST(1)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
     const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
     __syncthreads();
     LWF_ST(0)
     fln<NC>(XD, ldD, Ld, D, n1, XD, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
-    fgemm<0, FIX ? 128 : 0, FIX ? 64 : 0>(blob, pw, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->cq, XD, ldD, 0, Ld, QC, ldH, nullptr, 0, 0);
+    fgemm<BF, 0, FIX ? 128 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
     fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
     __syncthreads();
     LWF_ST(1)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
     const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
     __syncthreads();
     LWF_ST(0)
     fln<NC>(XD, ldD, Ld, D, n2, XD, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
     __syncthreads();
     LWF_ST(0)
-    fgemm<0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
     const LnPre<NC> n3 = lnpre<NC>(blob + ly->g3, blob + ly->b3, D);
     __syncthreads();
     LWF_ST(0)
@@ -647,7 +698,7 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   __syncthreads();
   LWF_ST(2)
   // projection of the last pred_len rows → out[b][pred][c_out]
-  fgemm<0, FIX ? 16 : 0, FIX ? 64 : 0>(blob, pw, p->proj, XD, ldD, 0, Ld, 0, 0, nullptr, 0, 0, out + (size_t)b * PV(pred) * PV(c_out), Ld - PV(pred),
+  fgemm<BF, 0, FIX ? 16 : 0, FIX ? 64 : 0>(blob, pw, pwb, p->proj, XD, ldD, 0, Ld, 0, 0, nullptr, 0, 0, out + (size_t)b * PV(pred) * PV(c_out), Ld - PV(pred),
            PV(c_out));
   LWF_ST(0)
   LWF_ST_END
@@ -656,10 +707,12 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
 }
 
 // the instance of a plan: four LayerNorm chunks per lane row up to d_model 64, sixteen up to 256
-static const void* kernel_of(int D, bool fix) {
-  if (fix) return reinterpret_cast<const void*>(lw_fused<4, true>);
-  return D <= 64 ? reinterpret_cast<const void*>(lw_fused<4>) : reinterpret_cast<const void*>(lw_fused<16>);
+template <bool BF>
+static const void* kernel_of_t(int D, bool fix) {
+  if (fix) return reinterpret_cast<const void*>(lw_fused<4, true, BF>);
+  return D <= 64 ? reinterpret_cast<const void*>(lw_fused<4, false, BF>) : reinterpret_cast<const void*>(lw_fused<16, false, BF>);
 }
+static const void* kernel_of(int D, bool fix, bool bf) { return bf ? kernel_of_t<true>(D, fix) : kernel_of_t<false>(D, fix); }
 
 bool plan_is_d64(const FPlan& p) {
   using Q = D64Plan;
@@ -681,20 +734,19 @@ bool plan_is_d64(const FPlan& p) {
   return ok;
 }
 
-int prepare_fused(int D, bool fix) {
-  return cet::ensure_lds_attr(kernel_of(D, fix)) ? 0 : -1;
+int prepare_fused(int D, bool fix, bool bf) {
+  return cet::ensure_lds_attr(kernel_of(D, fix, bf)) ? 0 : -1;
 }
 
-int launch_fused(const FPlan* d_plan, int D, bool fix, size_t lds_bytes, const float* blob, const float* pw,
-                 const float* x_enc, const float* x_dec, float* out, const int32_t* idx, int B, hipStream_t st) {
+int launch_fused(const FPlan* d_plan, int D, bool fix, bool bf, size_t lds_bytes, const float* blob, const float* pw,
+                 const void* pwb_, const float* x_enc, const float* x_dec, float* out, const int32_t* idx, int B,
+                 hipStream_t st) {
   if (B <= 0) return 0;
-  if (prepare_fused(D, fix)) return -1;
-  if (fix)
-    hipLaunchKernelGGL((lw_fused<4, true>), dim3(B), dim3(NTH), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
-  else if (D <= 64)
-    hipLaunchKernelGGL(lw_fused<4>, dim3(B), dim3(NTH), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
-  else
-    hipLaunchKernelGGL(lw_fused<16>, dim3(B), dim3(NTH), lds_bytes, st, d_plan, blob, pw, x_enc, x_dec, out, idx);
+  if (prepare_fused(D, fix, bf)) return -1;
+  const bf16x8* pwb = reinterpret_cast<const bf16x8*>(pwb_);
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(const FPlan*, const float*, const float*, const bf16x8*, const float*,
+                                               const float*, float*, const int32_t*)>(const_cast<void*>(kernel_of(D, fix, bf))),
+                     dim3(B), dim3(NTH), lds_bytes, st, d_plan, blob, pw, pwb, x_enc, x_dec, out, idx);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

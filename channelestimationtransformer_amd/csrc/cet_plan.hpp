@@ -105,6 +105,9 @@ struct InformerPlan {
 //   [x_dec staged at entry] | [sampler state, in-kernel replay only]
 // Image rows: bf16 272 B ( 288 B — conflict-free ds_read_b128 — measured no faster), fp8
 // 144 B (conflict-free ds_read_b64).
+#ifdef CET_IMG_SWZ
+#define V4_RS16 288   // swizzled rows (cet_v4.hpp Img::off)
+#endif
 #ifndef V4_RS16
 #define V4_RS16 272   // A/B knob: bf16 image row stride (bytes); 288 (conflict-free ds_read_b128) measured equal
 #endif
@@ -121,7 +124,11 @@ constexpr int v4_ctx_bytes(int P) {
 }
 constexpr int v4_scr(int P) { return v4_ctx(P) + v4_ctx_bytes(P); }
 constexpr int v4_cnt(int P) { return v4_scr(P) + 8 * V2_SCR_FLOATS * 4; }   // multiplicity table, LMAX rows
-constexpr int v4_enc(int P) { return v4_cnt(P) + LMAX * 96; }               // stack output (plan-sized)
+// ProbSparse multiplicity-table rows: 96 count bytes (six key tiles) + 8 pad.  26 dwords ≡ 2 (mod 4): the
+// 16 query rows one lane group reads (attention phase A, 8-byte reads) fall on 16 distinct bank pairs; at
+// 96 bytes they fell on 4 (4-way, 24 extra LDS cycles per read; tools/probe/lds_probe.hip)
+constexpr int CNT_STRIDE = 104;
+constexpr int v4_enc(int P) { return v4_cnt(P) + LMAX * CNT_STRIDE; }       // stack output (plan-sized)
 static_assert(LMAX * LN3_STRIDE * 4 + LMAX * 8 <= 8 * V2_SCR_FLOATS * 4,
               "LN partials and row statistics fit the scratch they alias");
 static_assert(v4_ctx(0) % 16 == 0 && v4_scr(0) % 16 == 0 && v4_enc(1) % 16 == 0 && v4_enc(2) % 16 == 0, "16-B");

@@ -57,11 +57,6 @@ struct Geo {
   static constexpr int IMG = LMAX * RS;                // one plane of a LMAX-row image
 };
 
-#ifdef CET_AB8_DUMP
-// diagnostic (round-5 investigation of the ab8 candidate): head 0 of workgroup 0's first 6-tile attention call
-// writes its K/V tiles, the first selected tile's softmax statistics and context to this array
-__device__ unsigned int g_ab8_dump[8][128 * 64];   // per head
-#endif
 // ------------------------------------------------------------------ fragments and products
 template <int P>
 struct XF {  // B-role (activation) fragment of one 16x16x32 k-step
@@ -232,6 +227,25 @@ struct Img : ImgBase<P> {
     (void)l;
   }
   __device__ __forceinline__ Img() = default;
+#ifdef CET_IMG_SWZ
+  static constexpr bool SWZ = P != P_FP8;
+#else
+  static constexpr bool SWZ = false;
+#endif
+  // byte offset of (row, byte) in a plane.  SWZ (RS = 288): byte bits 4-5 XOR-ed with row bits 2-3.  The
+  // 32-byte row skew alone makes an MFMA operand read (ds_read_b128: lanes of rows c = 0-15 over two adjacent
+  // 16-byte chunks per lane group) conflict-free but the image writes (ds_write_b64: 16 rows, one column, 32
+  // banks) 4-way; the XOR spreads those rows back to 2-way and keeps the reads conflict-free
+  // (tools/lds_bank_model.py, tools/probe/lds_probe.hip).  It touches neither bit 6-7 (the k-step, an
+  // immediate offset) nor, for rows mt·16 + c, anything but c: one per-lane term per access pattern.  A view
+  // must start on a row ≡ 0 (mod 16) of its image (ImgRows shifts rows instead)
+  static __device__ __forceinline__ int off(int row, int byte) {
+    constexpr int RS = Geo<P>::RS;
+    // spelled so that the XOR sees only the lane-dependent parts (byte bits 4-5, row bits 2-3): for rows
+    // mt·16 + c and bytes ks·64 + 16g the term is one per-lane value and mt, ks stay immediate offsets
+    if constexpr (SWZ) return row * RS + (byte & ~48) + ((byte & 48) ^ ((row << 2) & 48));
+    return row * RS + byte;
+  }
   __device__ __forceinline__ XF<P> ld(int row, int k0) const {
     constexpr int RS = Geo<P>::RS;
 #ifdef CET_ABL_LDSROW
@@ -247,8 +261,9 @@ struct Img : ImgBase<P> {
       r.q = *reinterpret_cast<const long*>(base + row * RS + k0);
 #endif
     } else {
-      r.h = *reinterpret_cast<const bf16x8*>(base + row * RS + 2 * k0);
-      if constexpr (P == P_X3) r.l = *reinterpret_cast<const bf16x8*>(base + lo + row * RS + 2 * k0);
+      const int o = off(row, 2 * k0);
+      r.h = *reinterpret_cast<const bf16x8*>(base + o);
+      if constexpr (P == P_X3) r.l = *reinterpret_cast<const bf16x8*>(base + lo + o);
     }
     return r;
   }
@@ -258,9 +273,9 @@ struct Img : ImgBase<P> {
       *reinterpret_cast<uint32_t*>(base + row * RS + n0) = fp8x4(v);
     } else {
       const bf16x4 h = cvt4(v);
-      *reinterpret_cast<bf16x4*>(base + row * RS + 2 * n0) = h;
-      if constexpr (P == P_X3)
-        *reinterpret_cast<bf16x4*>(base + lo + row * RS + 2 * n0) = cvt4(v - __builtin_convertvector(h, f32x4));
+      const int o = off(row, 2 * n0);
+      *reinterpret_cast<bf16x4*>(base + o) = h;
+      if constexpr (P == P_X3) *reinterpret_cast<bf16x4*>(base + lo + o) = cvt4(v - __builtin_convertvector(h, f32x4));
     }
   }
   __device__ __forceinline__ void st1(int row, int n, float v) const {
@@ -269,10 +284,19 @@ struct Img : ImgBase<P> {
       *reinterpret_cast<uint8_t*>(base + row * RS + n) = (uint8_t)__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false);
     } else {
       const __bf16 h = (__bf16)v;
-      *reinterpret_cast<__bf16*>(base + row * RS + 2 * n) = h;
-      if constexpr (P == P_X3) *reinterpret_cast<__bf16*>(base + lo + row * RS + 2 * n) = (__bf16)(v - (float)h);
+      const int o = off(row, 2 * n);
+      *reinterpret_cast<__bf16*>(base + o) = h;
+      if constexpr (P == P_X3) *reinterpret_cast<__bf16*>(base + lo + o) = (__bf16)(v - (float)h);
     }
   }
+};
+
+// rows r0 .. of an image as a writer's rows 0 .. (the encoder norm's rows of the stack output)
+template <int P>
+struct ImgRows {
+  Img<P> im;
+  int r0;
+  __device__ __forceinline__ void st4(int row, int n0, const f32x4& v) const { im.st4(row + r0, n0, v); }
 };
 
 // B-operand loaders
@@ -574,6 +598,63 @@ __device__ __forceinline__ void gemm_kouter_res(const WPre<P, KH>& p, const Mem&
   for (int mt = 0; mt < NMT; ++mt) epi(mt, n0, c[mt] * sc + bi);
 }
 
+// One-pass LayerNorm, step 1: each wave publishes (Σx, Σx²) over its 16 features per row.  The two
+// butterflies share their swaps: permlane16_swap(s, q) leaves rows (s0+s1, q0+q1, s2+s3, q2+q3) after one
+// add, and the 32-lane swap then gives Σs in rows 0 / 2 and Σq in rows 1 / 3 — lanes g and g + 2 store the
+// same word to the same address, so the publish needs no branch.
+template <int N>
+__device__ __forceinline__ void ln_publish(const Res<N>& X, int nmt, float* part) {
+  const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      const f32x4 x = X.v[mt];
+      // on the fragment's natural register pairs: packed math with no operand moves
+      const f32x2 hs = x.xy + x.zw, hq = x.xy * x.xy + x.zw * x.zw;
+      const float s = hs.x + hs.y, q = hq.x + hq.y;
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(q), false, false);
+      const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+      const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+      part[(mt * 16 + c) * LN_STRIDE + 2 * w + (g & 1)] = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+    }
+  }
+}
+
+// row statistics (mean, 1/std) of row m from the 8 waves' (Σx, Σx²)
+__device__ __forceinline__ f32x2 ln_row_stats(const float* part, int m, float eps, bool unbiased_std) {
+  const float* pr = part + m * LN_STRIDE;
+  const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
+  // (Σx, Σx²) pairs summed as pairs (packed adds on the loaded register pairs)
+  const f32x2 t = ((p0.xy + p0.zw) + (p1.xy + p1.zw)) + ((p2.xy + p2.zw) + (p3.xy + p3.zw));
+  const float sx = t.x, sq = t.y;
+  const float mean = sx * (1.0f / 128.0f);
+  const float M2 = fmaxf(fmaf(-sx, mean, sq), 0.f);   // Σx² − (Σx)²/128
+  const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
+                                 : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
+  return f32x2{mean, inv};
+}
+
+// step 2 in the own-rows form: every wave combines the partials of the rows it holds and normalises them
+template <int N, class Out, class Out2, bool INPLACE = true>
+__device__ __forceinline__ void ln_apply_own(Res<N>& X, int nmt, int rows, f32x4 g0, f32x4 b0, float eps,
+                                             bool unbiased_std, const float* part, const Out& out, const Out2* out2) {
+  const int lane = lane_op(), w = wave_id(), c = lane & 15;
+  const int nb = 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      const int m = mt * 16 + c;
+      const f32x2 st = ln_row_stats(part, m, eps, unbiased_std);
+      const f32x4 y = (X.v[mt] - st[0]) * st[1] * g0 + b0;
+      if (INPLACE) X.v[mt] = y;
+      if (m < rows) {
+        out.st4(m, nb, y);
+        if (out2) out2->st4(m, nb, y);
+      }
+    }
+  }
+}
+
 // LayerNorm of the register residual over all 128 features (8 waves × 16).
 //   1. each wave reduces its 16 features per row to (Σx, Σx²) and stores the pair (LDS partials);
 //   2. wave w < nmt combines the 8 pairs of the rows of m-tile w into (mean, 1/std) per row — once per
@@ -592,37 +673,9 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
   const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
 #ifndef CET_LN_TWOPASS
-  // One pass: each wave publishes (Σx, Σx²) over its 16 features per row.  The two butterflies share
-  // their swaps: permlane16_swap(s, q) leaves rows (s0+s1, q0+q1, s2+s3, q2+q3) after one add, and the
-  // 32-lane swap then gives Σs in rows 0 / 2 and Σq in rows 1 / 3 — lanes g and g + 2 store the same
-  // word to the same address, so the publish needs no branch.
-#pragma unroll
-  for (int mt = 0; mt < N; ++mt) {
-    if (mt < nmt) {
-      const f32x4 x = X.v[mt];
-      // on the fragment's natural register pairs: packed math with no operand moves
-      const f32x2 hs = x.xy + x.zw, hq = x.xy * x.xy + x.zw * x.zw;
-      const float s = hs.x + hs.y, q = hq.x + hq.y;
-      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(q), false, false);
-      const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-      const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
-      part[(mt * 16 + c) * LN_STRIDE + 2 * w + (g & 1)] = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
-    }
-  }
+  ln_publish(X, nmt, part);
   __syncthreads();
-  // row statistics (mean, 1/std) of row m from the 8 waves' (Σx, Σx²)
-  auto row_stats = [&](int m) __attribute__((always_inline)) {
-    const float* pr = part + m * LN_STRIDE;
-    const f32x4 p0 = load4(pr), p1 = load4(pr + 4), p2 = load4(pr + 8), p3 = load4(pr + 12);
-    // (Σx, Σx²) pairs summed as pairs (packed adds on the loaded register pairs)
-    const f32x2 t = ((p0.xy + p0.zw) + (p1.xy + p1.zw)) + ((p2.xy + p2.zw) + (p3.xy + p3.zw));
-    const float sx = t.x, sq = t.y;
-    const float mean = sx * (1.0f / 128.0f);
-    const float M2 = fmaxf(fmaf(-sx, mean, sq), 0.f);   // Σx² − (Σx)²/128
-    const float inv = unbiased_std ? __builtin_amdgcn_rcpf(sqrtf(M2 * (1.0f / 127.0f)) + eps)
-                                   : __builtin_amdgcn_rsqf(M2 * (1.0f / 128.0f) + eps);
-    return f32x2{mean, inv};
-  };
+  auto row_stats = [&](int m) __attribute__((always_inline)) { return ln_row_stats(part, m, eps, unbiased_std); };
 #ifndef CET_LN_TWO_BARRIER
 #ifndef CET_LN_ONE_MAX
 #define CET_LN_ONE_MAX 1
@@ -632,19 +685,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     // barrier; the caller's barrier after the LN orders these reads before the partials are rewritten.
     // For the encoder's 3-6 tiles the redundant combining costs more than the barrier it saves
     // (-DCET_LN_ONE_MAX=3 ±0, =6 +1.2 us; profiles/r04/ab9/ab.log)
-#pragma unroll
-    for (int mt = 0; mt < N; ++mt) {
-      if (mt < nmt) {
-        const int m = mt * 16 + c;
-        const f32x2 st = row_stats(m);
-        const f32x4 y = (X.v[mt] - st[0]) * st[1] * g0 + b0;
-        if (INPLACE) X.v[mt] = y;
-        if (m < rows) {
-          out.st4(m, nb, y);
-          if (out2) out2->st4(m, nb, y);
-        }
-      }
-    }
+    ln_apply_own<N, Out, Out2, INPLACE>(X, nmt, rows, g0, b0, eps, unbiased_std, part, out, out2);
     return;
   }
 #endif
@@ -699,6 +740,24 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
       }
     }
   }
+}
+
+// Two torch.nn.LayerNorms under one barrier, both in the own-rows form: the fused decoder layer 0's LN1
+// (decoder.py:31) beside the last encoder layer's LN1 (encoder.py:50) in the shape instances.  Each has its
+// own partials; the caller's barrier after it orders the reads before either is rewritten.
+template <int N1, int N2, class O1, class O2>
+__device__ __forceinline__ void ln_res_pair(Res<N1>& X1, int nmt1, int rows1, const LNDesc ln1, float* part1,
+                                            const O1& out1, Res<N2>& X2, int nmt2, int rows2, const LNDesc ln2,
+                                            float* part2, const O2& out2, const Mem& mm, float eps) {
+  const int lane = lane_op(), w = wave_id();
+  const int nb = 16 * w + 4 * (lane >> 4);
+  const f32x4 g1 = pload4(mm, ln1.g, nb), b1 = pload4(mm, ln1.b, nb);
+  const f32x4 g2 = pload4(mm, ln2.g, nb), b2 = pload4(mm, ln2.b, nb);
+  ln_publish(X1, nmt1, part1);
+  ln_publish(X2, nmt2, part2);
+  __syncthreads();
+  ln_apply_own<N1, O1, O1>(X1, nmt1, rows1, g1, b1, eps, false, part1, out1, (const O1*)nullptr);
+  ln_apply_own<N2, O2, O2>(X2, nmt2, rows2, g2, b2, eps, false, part2, out2, (const O2*)nullptr);
 }
 
 // image of the register residual (rows < rows)
@@ -921,8 +980,7 @@ template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false, bool NKX = false
 __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
                                                const AF<plain_of<PD>()>* kin = nullptr,
                                                const AF<plain_of<PD>()>* vin = nullptr,
-                                               const WPre<PD, 4>* qpre = nullptr,
-                                               const KVPre<PD>* kvpre = nullptr) {
+                                               const WPre<PD, 4>* qpre = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -959,33 +1017,10 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       Kf[mt] = kin[mt];
       Vf[mt] = vin[mt];
     }
-  } else if (kvpre) {
-    project_kv<PD, MK>(io, *kvpre, Kf, Vf);   // weights requested by the caller (CET_AB8 experiment)
   } else {
     project_kv<PD, MK>(io, m, h, Kf, Vf);
   }
   SUB(1);
-#ifdef CET_AB8_DUMP
-  if constexpr (MQ == 6 && !EXTKV) {
-    if (blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u) {
-#pragma unroll
-      for (int t = 0; t < MK; ++t) {
-        const uint2 kh = __builtin_bit_cast(uint2, Kf[t].h), vh = __builtin_bit_cast(uint2, Vf[t].h);
-        g_ab8_dump[h][(4 * t + 0) * 64 + lane] = kh.x;
-        g_ab8_dump[h][(4 * t + 1) * 64 + lane] = kh.y;
-        g_ab8_dump[h][(4 * t + 2) * 64 + lane] = vh.x;
-        g_ab8_dump[h][(4 * t + 3) * 64 + lane] = vh.y;
-        if constexpr (PA == P_X3) {
-          const uint2 kl = __builtin_bit_cast(uint2, Kf[t].l), vl = __builtin_bit_cast(uint2, Vf[t].l);
-          g_ab8_dump[h][(24 + 4 * t + 0) * 64 + lane] = kl.x;
-          g_ab8_dump[h][(24 + 4 * t + 1) * 64 + lane] = kl.y;
-          g_ab8_dump[h][(24 + 4 * t + 2) * 64 + lane] = vl.x;
-          g_ab8_dump[h][(24 + 4 * t + 3) * 64 + lane] = vl.y;
-        }
-      }
-    }
-  }
-#endif
   // Q tiles are projected where they are consumed (per query tile in M, per selected tile in the
   // softmax): wq and its epilogue vectors are the only Q state that lives
   if constexpr (!EARLYQ) {
@@ -1182,33 +1217,6 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
     sum = xor_sum(sum, 16);
     sum = xor_sum(sum, 32);
     const float inv = __builtin_amdgcn_rcpf(sum);
-#ifdef CET_AB8_DUMP
-    if constexpr (MQ == 6 && !EXTKV) {
-      if (blockIdx.x == 0 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u) {
-        g_ab8_dump[h][(64 + 8 * st + 0) * 64 + lane] = __float_as_uint(mx);
-        g_ab8_dump[h][(64 + 8 * st + 1) * 64 + lane] = __float_as_uint(sum);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) g_ab8_dump[h][(64 + 8 * st + 2 + r) * 64 + lane] = __float_as_uint(o[r]);
-        g_ab8_dump[h][(64 + 8 * st + 6) * 64 + lane] = (unsigned)qi;
-      }
-      if (blockIdx.x == 0 && st == 0 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u) {
-        const uint2 qh = __builtin_bit_cast(uint2, qs.h);
-        g_ab8_dump[h][48 * 64 + lane] = qh.x;
-        g_ab8_dump[h][49 * 64 + lane] = qh.y;
-        g_ab8_dump[h][50 * 64 + lane] = __float_as_uint(mx);
-        g_ab8_dump[h][51 * 64 + lane] = __float_as_uint(sum);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) g_ab8_dump[h][(52 + r) * 64 + lane] = __float_as_uint(o[r]);
-        if constexpr (PA == P_X3) {
-          const uint2 ql = __builtin_bit_cast(uint2, qs.l);
-          g_ab8_dump[h][56 * 64 + lane] = ql.x;
-          g_ab8_dump[h][57 * 64 + lane] = ql.y;
-        }
-      }
-      if (blockIdx.x == 0 && st == nst - 1 && __builtin_amdgcn_readfirstlane(g_ab8_dump[h][127 * 64]) == 0u)
-        g_ab8_dump[h][127 * 64 + lane] = 1u;   // written once per launch sequence (the host clears it)
-    }
-#endif
     if (i < nsel) {
       ctx_st4(qi, g * 4, o * inv);
       if (io.attn_out) {

@@ -147,7 +147,10 @@ int cet_last_kernel(cet_engine* e, char* name, int buflen);
  *    3 (reported only) the layer-wise engine: models the fused kernels cannot carry (d_model != 128,
  *      n_heads != 8, d_ff > 128, more than 96 encoder / 48 decoder rows; up to d_model 1024 and 128
  *      rows) run as one launch per operator with fp32 operands on the f32 MFMA (cet_lw.hip).
- *      CET_LAYERWISE=1 in the environment at cet_create_informer routes any model there.
+ *      CET_LAYERWISE=1 in the environment at cet_create_informer routes any model there.  On such an
+ *      engine "auto" keeps fp32 and 0 selects bf16 GEMM operands (fp32 accumulation, LayerNorm and
+ *      attention) in its fused one-launch form (cet_lwf.hip; feature counts multiples of 8): a forward
+ *      outside that form then fails with CET_E_INVALID; 1 and 2 are refused.
  * cet_get_precision() returns the precision the packed plan uses (packs the weights if needed).
  * Replaces nothing in the reference, which computes in fp32 (FullPrecision/InformerModel) or with
  * fp32 fake-quantised weights (models/InformerLSQ/LSQ.py:65-74). */

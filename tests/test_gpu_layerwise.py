@@ -331,3 +331,75 @@ def test_fused_layerwise_stack_output_rows_bound(seq_len, path):
     assert m.engine(dev).last_path() == path
     ref, _ = orc.forward(xe, xd, ())
     assert rel_nmse(out, ref) < TOL, rel_nmse(out, ref)
+
+
+BF16_TOL = 1e-4   # the north star's tolerance (BASELINE.json) for bf16 operands
+
+
+@pytest.mark.parametrize("B", [1, 512])
+def test_fused_layerwise_bf16_checkpoint_vs_oracle(B):
+    """bf16 GEMM operands in the fused layer-wise form (cet_set_precision "bf16" on a layer-wise engine; the
+    compile-time d_model-64 instance, v_mfma_f32_16x16x32_bf16 with fp32 accumulation, LayerNorm and
+    attention): the checkpoint fixture against the reference's own output and a random batch's row slices
+    against the float64 oracle, both within the north star's 1e-4 — and above the fp32 bar, so the bf16
+    instance is the one that ran —; a repeated forward bit for bit."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case(CKPT)
+    m = model_for(case)
+    eng = m.engine(torch.device("cuda:0"))
+    eng.set_precision("bf16")
+    assert eng.precision() == "bf16"
+    out, _, _ = run_engine(m, case.z["x_enc"], case.z["x_dec"], case.idx)
+    assert eng.last_path() == "layerwise-fused"
+    assert eng.last_kernel() == "cet::lw::lw_fused (bf16 operands)"
+    err = rel_nmse(out, case.z["out"])
+    assert TOL < err < BF16_TOL, err
+    xe, xd = _random_batch(case.cfg, B, 300 + B)
+    out, _, _ = run_engine(m, xe, xd, case.idx)
+    again, _, _ = run_engine(m, xe, xd, case.idx)
+    np.testing.assert_array_equal(out, again)
+    rows = np.r_[0:32, B - 32:B] if B > 64 else np.arange(B)
+    ref, _ = oracle_for(case).forward(xe[rows], xd[rows], case.idx)
+    err = rel_nmse(out[rows], ref)
+    assert err < BF16_TOL, err
+
+
+def test_fused_layerwise_bf16_runtime_shapes_and_refusals():
+    """The bf16 operands on the runtime-shape instance (seq_len 48: three m-tiles per GEMM, 48 selected rows
+    — the one-lane-per-row softmax —, a 34-row decoder) against the float64 oracle within 1e-4, attn "full":
+    with a genuinely sparse ProbSparse call bf16 rounding of the scores can flip the top-u selection, an
+    output discontinuity no operand precision short of fp32 bounds (measured 0.12 on a sparse causal decoder;
+    the v4 kernel's "auto" takes split bf16 there).  A forward that materialises attention maps
+    (operator launches only) is refused, not run in fp32; "auto" stays fp32."""
+    _gpu()
+    import dataclasses
+
+    from engine_util import model_for, run_engine
+
+    from channelestimationtransformer_amd.rng import draw_indices
+    from oracle.informer_np import sample_shapes
+
+    base = load_case(CKPT)
+    meta = dict(base.meta)
+    meta["cfg"] = dict(base.cfg, attn="full", seq_len=48, label_len=25, pred_len=9)
+    case = dataclasses.replace(base, meta=meta)
+    orc = oracle_for(case)
+    idx = draw_indices(sample_shapes(orc.cfg), seed=13)
+    assert not len(idx)   # attn "full": no draws
+    m = model_for(case)
+    eng = m.engine(torch.device("cuda:0"))
+    assert eng.precision() == "fp32-layerwise"
+    eng.set_precision("bf16")
+    xe, xd = _random_batch(case.cfg, 41, 17)
+    out, _, _ = run_engine(m, xe, xd, idx)
+    assert eng.last_path() == "layerwise-fused"
+    assert eng.last_kernel() == "cet::lw::lw_fused (bf16 operands)"
+    ref, _ = orc.forward(xe, xd, idx)
+    err = rel_nmse(out, ref)
+    assert TOL < err < BF16_TOL, err
+    with pytest.raises(Exception, match="bf16 operands need the fused"):
+        run_engine(m, xe, xd, idx, attns=True)
+    with pytest.raises(Exception):
+        eng.set_precision("split-bf16")

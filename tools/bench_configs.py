@@ -44,9 +44,9 @@ from oracle.transformer_np import TransformerConfig, TransformerOracle  # noqa: 
 PEAK = {"bf16": 2500.0, "fp8": 5000.0, "fp32": 157.3}   # dense MFMA TFLOP/s (MI355X_MICROARCH.md chip table)
 
 
-def informer(dev, e_layers, attn, lsq_bits=0, seq_len=90, d_model=128):
-    args = [16, 16, 16, seq_len, 10, 5, 5, d_model, 8, e_layers, 3, 64, 0.05, attn, "fixed", "gelu", False, True,
-            dev]
+def informer(dev, e_layers, attn, lsq_bits=0, seq_len=90, d_model=128, label_len=10):
+    args = [16, 16, 16, seq_len, label_len, 5, 5, d_model, 8, e_layers, 3, 64, 0.05, attn, "fixed", "gelu", False,
+            True, dev]
     m = InformerStackLSQ(*args, lsq_bits) if lsq_bits else InformerStack(*args)
     spec = m._schema()
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(spec, 0).items()},
@@ -54,8 +54,8 @@ def informer(dev, e_layers, attn, lsq_bits=0, seq_len=90, d_model=128):
     if lsq_bits:
         m.enable_lsq(lsq_bits)
     state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
-    orc = InformerOracle(InformerConfig(seq_len=seq_len, d_model=d_model, e_layers=tuple(e_layers), attn=attn,
-                                        lsq_bits=lsq_bits or None), state)
+    orc = InformerOracle(InformerConfig(seq_len=seq_len, label_len=label_len, d_model=d_model,
+                                        e_layers=tuple(e_layers), attn=attn, lsq_bits=lsq_bits or None), state)
     return m.eval(), orc
 
 
@@ -73,8 +73,8 @@ def run(m, orc, dev, B, steps, variant=None, precision=None, settle_s=1.0, m2=No
         eng.set_variant(variant)
     if precision is not None:
         eng.set_precision(precision)
-    xe_np, xd_np, _ = make_batch(B, seed=7, seq_len=orc.cfg.seq_len) if isinstance(orc, InformerOracle) else \
-        make_batch(B, seed=7)
+    xe_np, xd_np, _ = make_batch(B, seed=7, seq_len=orc.cfg.seq_len, label_len=orc.cfg.label_len) \
+        if isinstance(orc, InformerOracle) else make_batch(B, seed=7)
     xe, xd = torch.from_numpy(xe_np).to(dev), torch.from_numpy(xd_np).to(dev)
     out = torch.empty(B, 5, 16, device=dev)
     prob = bool(eng.prob_calls())
@@ -156,6 +156,11 @@ def main():
         ("d64 MimoSimulation checkpoint architecture (d_model 64, seq_len 25, e_layers=[4,3], attn=full), "
          "fused layer-wise form", lambda: informer(dev, [4, 3], "full", seq_len=25, d_model=64), 512,
          informer_flops(seq_len=25, d_model=64, e_layers=(4, 3), attn="full"), {}, "fp32"),
+        ("d64 MimoSimulation checkpoint architecture (d_model 64, seq_len 25, e_layers=[4,3], attn=full), "
+         "fused layer-wise form, bf16 operands", lambda: informer(dev, [4, 3], "full", seq_len=25, d_model=64), 512,
+         informer_flops(seq_len=25, d_model=64, e_layers=(4, 3), attn="full"), dict(precision="bf16"), "bf16"),
+        ("lab20 FullPrecision InformerStack label_len=20 (sparse 25-row decoder; auto precision: split bf16)",
+         lambda: informer(dev, [4], "prob", label_len=20), 512, informer_flops(label_len=20), {}, "bf16"),
     ]
     tol = {"fp8": 2e-3}   # rel-NMSE bar: north_star's 1e-4, the self-set fp8 bar for C5 fp8
     for name, mk, B, flops, kw, peak in runs:
