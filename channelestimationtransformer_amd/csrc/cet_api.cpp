@@ -408,39 +408,6 @@ struct Packer {
     d.scale = scale ? vec(scale, N, Np) : NONE;
     return d;
   }
-#ifdef CET_FP8_SCALED
-  // An LSQ integer grid q ∈ [−128, 127] for the block-scaled fp8 MFMA (v4 P_FP8, cet_v4.hpp): per
-  // 64-feature block kb, byte j = 8b + i of the lane's 32 carries feature 64·kb + 32·(b&1) + 8(lane>>4) + i
-  // as hi = ⌊q/16⌋ (bytes 0-15, the MFMA's scale blocks 0-1, ×2^4) or lo = q mod 16 (bytes 16-31, blocks
-  // 2-3, ×2^0), all e4m3-exact; the hi half and the lo half are stored as the 16-byte fragments of
-  // k-steps 2·kb and 2·kb + 1, so the blob keeps the bf16 geometry (16 B per lane per 32-feature k-step,
-  // 1 KiB per wave load).
-  GemmDesc gemm_fp8(const std::vector<float>& q, int N, int K, const float* bias, const float* scale) {
-    GemmDesc d{};
-    const int Np = r16(N), Kp = (K + 63) & ~63;
-    d.w = (uint32_t)(wb.size() / 8);
-    d.n = (uint16_t)Np;
-    d.k = (uint16_t)Kp;
-    for (int nt = 0; nt < Np / 16; ++nt)
-      for (int kb = 0; kb < Kp / 64; ++kb)
-        for (int h = 0; h < 2; ++h)
-          for (int lane = 0; lane < 64; ++lane) {
-            const int g = lane >> 4, n = nt * 16 + (lane & 15);
-            uint8_t by[16];
-            for (int j = 0; j < 16; ++j) {
-              const int b = 2 * h + (j >> 3);   // scale block of this byte
-              const int k = kb * 64 + 32 * (b & 1) + 8 * g + (j & 7);
-              const int v = n < N && k < K ? (int)q[(size_t)n * K + k] : 0;
-              const int hi = (int)std::floor(v / 16.0);
-              by[j] = f2e4m3((float)(b < 2 ? hi : v - 16 * hi));
-            }
-            for (int j = 0; j < 8; ++j) wb.push_back((uint16_t)(by[2 * j] | (by[2 * j + 1] << 8)));
-          }
-    d.bias = bias ? vec(bias, N, Np) : NONE;
-    d.scale = scale ? vec(scale, N, Np) : NONE;
-    return d;
-  }
-#else
   // An LSQ integer grid q ∈ [−128, 127] as e4m3 pairs (v4 P_FP8, default form): lane fragment = 8 bytes
   // of 16·⌊q/16⌋ then 8 bytes of q mod 16, both exact in e4m3; same 16 B per lane per k-step as bf16.
   GemmDesc gemm_fp8(const std::vector<float>& q, int N, int K, const float* bias, const float* scale) {
@@ -466,7 +433,6 @@ struct Packer {
     d.scale = scale ? vec(scale, N, Np) : NONE;
     return d;
   }
-#endif
   uint32_t vec(const float* v, int n, int npad) {
     while (pb.size() % 4) pb.push_back(0.f);
     const uint32_t off = (uint32_t)pb.size();

@@ -64,6 +64,9 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     a.stamps[(size_t)b * MAX_STAMPS + 127] = __builtin_amdgcn_s_memtime();
     // the constant 100 MHz clock, comparable across workgroups and XCDs (s_memtime is not)
     a.stamps[(size_t)b * MAX_STAMPS + 98] = __builtin_amdgcn_s_memrealtime();
+    // where it ran: HW_ID (wave / SIMD / CU / SH / SE fields) and XCC_ID, hwreg(id, 0, 32)
+    a.stamps[(size_t)b * MAX_STAMPS + 96] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    a.stamps[(size_t)b * MAX_STAMPS + 97] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
   const int C = PL.C, L0 = PL.seq_len, CS = PL.in_stride, Ld = PL.dec_len;
   // this sequence's x_enc rows are requested first (one f32x4 per thread: L·C/4 ≤ 384), so their HBM
@@ -155,7 +158,24 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   Res<MT> X;
   unsigned long long* stamps = (DIAG || ST) && a.stamps ? a.stamps + (size_t)b * MAX_STAMPS : nullptr;
   int sid = 0;
+#ifdef CET_PRIO_SLICE
+  // The two workgroups of a CU (blocks b and b + 256 at B = 512, tools/stamps.py) compete for VALU issue,
+  // which goes to the older waves first: one finishes ≈21 µs before the other, which then runs alone on a
+  // half-idle CU.  At every phase boundary each workgroup takes the high priority in alternate slices of
+  // 2^CET_PRIO_SLICE ticks of the 100 MHz chip clock, the younger in the odd slices, so both progress alike.
+  const unsigned young = ((unsigned)b >> 8) & 1u;
+  auto prio = [&]() {
+    const unsigned rt = (unsigned)__builtin_amdgcn_s_memrealtime();
+    if (((rt >> CET_PRIO_SLICE) ^ young) & 1u)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+  };
+#else
+  auto prio = [&]() {};
+#endif
   auto STAMP = [&]() {
+    prio();
     if (stamps) {
       if (threadIdx.x == 0 && sid < MAX_STAMPS) stamps[sid] = __builtin_amdgcn_s_memtime();
       ++sid;

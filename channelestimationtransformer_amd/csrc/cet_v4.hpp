@@ -9,28 +9,21 @@
 //   P_FP8   OCP e4m3 activations for the LSQ-quantised layers, the integer weight grid
 //           q ∈ [−128, 127] carried exactly in e4m3 parts, the step size in the epilogue.  Default:
 //           v_mfma_f32_16x16x32_fp8_fp8 with the grid as 16·⌊q/16⌋ and q mod 16, two MFMAs per
-//           32-feature k-step.  -DCET_FP8_SCALED: the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4,
-//           hi = ⌊q/16⌋ ∈ [−8, 7] and lo = q mod 16 in one MFMA per 64 features, the ×16 in the E8M0
-//           block scale (measured slower: the 8-register operand tuples spill the kernel).
+//           32-feature k-step.  (The block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 form — hi and lo in
+//           one MFMA per 64 features, the ×16 in the E8M0 block scale — was removed in round 5: its
+//           8-register operand tuples spill ≈270 VGPRs at the 128-VGPR cap and it ran C5 fp8 at 263.6 vs
+//           219.3 µs, profiles/r05/fp8_scaled/; its lane/byte/scale layout, probed on MI355X, is kept in
+//           tools/probe/mfma_scale_probe.hip and profiles/r03/mfma_scale_probe.txt.)
 //           The layers the reference does not quantise (token embedding, projection) and the attention
 //           products stay bf16.
 //
-// Fragment geometry: bf16 / split bf16 use v_mfma_f32_16x16x32_* (lane l holds A[row l&15]
-// [k = 8(l>>4) .. +7] and B[k = 8(l>>4) .. +7][col l&15]), as does the default fp8 form
-// (v_mfma_f32_16x16x32_fp8_fp8: 8 e4m3 per lane).  The CET_FP8_SCALED form is the 16x16x128 block-scaled one.
-// Probed on MI355X (tools/probe/mfma_scale_probe.hip, profiles/r03/mfma_scale_probe.txt): byte j of
-// lane l carries K index 16(l>>4) + j for j < 16 and 64 + 16(l>>4) + (j − 16) for j ≥ 16, and scale
-// block b = K/32 of row (col) r takes its E8M0 byte from lane r + 16b — so bytes 0-15 of every lane lie
-// in blocks 0-1 (scales from lanes 0-31) and bytes 16-31 in blocks 2-3 (lanes 32-63).  Bytes 0-15 carry
-// hi (×2^4) and bytes 16-31 lo (×2^0) of the real features 64·kb + 32·((j>>3)&1) + 8(l>>4) + (j&7), in
-// the same byte order in both operands (the products pair up whatever K index a byte denotes), so a
-// lane's activation bytes are two 8-byte runs (k0 and k0 + 32) repeated twice.  The weight blob keeps
-// 16 B per lane per 32-feature k-step for every policy, so the GEMM loops are shared: a scaled fp8 MFMA
-// consumes KR = 2 k-steps of weight fragments (the hi half, then the lo half).
+// Fragment geometry: every policy uses v_mfma_f32_16x16x32_* (lane l holds A[row l&15]
+// [k = 8(l>>4) .. +7] and B[k = 8(l>>4) .. +7][col l&15]; fp8: 8 e4m3 per lane).  The weight blob keeps
+// 16 B per lane per 32-feature k-step for every policy, so the GEMM loops are shared (KR = 1 k-step of
+// weight fragments per MFMA).
 //
-// Images (LDS): bf16 rows of 288 B (18 16-byte slots: the 16 lanes of every ds_read_b128 lane group
-// hit 16 distinct slots — conflict-free, MI355X_MICROARCH §LDS), X3 adds a lo plane, fp8 rows are
-// 144 B (conflict-free ds_read_b64).
+// Images (LDS): bf16 rows of 272 B (256 B of features + one 16-byte pad slot; -DCET_IMG_SWZ: 288 B with
+// a row-bit XOR, Img::off), X3 adds a lo plane, fp8 rows are 144 B (conflict-free ds_read_b64).
 #pragma once
 #include <type_traits>
 
@@ -74,19 +67,6 @@ template <>
 struct WF<P_X3> {
   bf16x8 h, l;
 };
-#ifdef CET_FP8_SCALED
-// ---- fp8 on the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (build with -DCET_FP8_SCALED; the
-//      packer follows the same macro): one MFMA per 64 features, hi and lo in one accumulator
-template <>
-struct XF<P_FP8> {
-  i32x8 q;   // 32 e4m3: features k0 .. +7 and k0 + 32 .. +7, twice (hi and lo blocks)
-};
-template <>
-struct WF<P_FP8> {
-  i32x4 q;   // 16 of the lane's 32 e4m3 weight bytes of one 64-feature block (hi or lo part)
-};
-constexpr bool FP8_SCALED = true;
-#else
 // ---- fp8 on v_mfma_f32_16x16x32_fp8_fp8 (default): per 32-feature k-step the grid as 16·⌊q/16⌋ and
 //      q mod 16 (both e4m3-exact), two MFMAs
 template <>
@@ -97,23 +77,16 @@ template <>
 struct WF<P_FP8> {
   long hi, lo;   // 16·⌊q/16⌋ and q mod 16, e4m3
 };
-constexpr bool FP8_SCALED = false;
-#endif
 
-// k-steps (32 features of weight fragments) one MFMA consumes, and the lane's activation k offset
+// k-steps (32 features of weight fragments) one MFMA consumes (one for every policy), and the lane's
+// activation k offset
 template <int P>
-constexpr int KR = P == P_FP8 && FP8_SCALED ? 2 : 1;
+constexpr int KR = 1;
 template <int P>
 __device__ __forceinline__ int kq_of(int lane) {
   return 8 * (lane >> 4);
 }
 
-// E8M0 block scales of the weight operand: lanes 0-31 give blocks 0-1 (bytes 0-15: hi = ⌊q/16⌋, ×2^4),
-// lanes 32-63 blocks 2-3 (bytes 16-31: lo, ×2^0)
-__device__ __forceinline__ int fp8_wscale() { return (threadIdx.x & 32) ? 127 : 131; }
-__device__ __forceinline__ i32x8 cat8(const i32x4& a, const i32x4& b) {
-  return i32x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
 __device__ __forceinline__ f32x4 mfma8(long a, long b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
 }
@@ -128,13 +101,8 @@ __device__ __forceinline__ f32x4 mma(const WF<P>* a, const XF<P>& b, f32x4 c) {
     c = mfma16x16x32(a->h, b.l, c);
     return mfma16x16x32(a->h, b.h, c);
   } else {
-#ifdef CET_FP8_SCALED
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cat8(a[0].q, a[1].q), b.q, c, 0, 0, 0, fp8_wscale(), 0,
-                                                            127);
-#else
     c = mfma8(a->lo, b.q, c);
     return mfma8(a->hi, b.q, c);
-#endif
   }
 }
 // X·Wᵀ (activations as A): V = X·Wvᵀ, whose C fragment is the A operand of Oᵀ = Vᵀ·Pᵀ
@@ -147,13 +115,8 @@ __device__ __forceinline__ f32x4 mma_xw(const XF<P>& a, const WF<P>* b, f32x4 c)
     c = mfma16x16x32(a.h, b->l, c);
     return mfma16x16x32(a.h, b->h, c);
   } else {
-#ifdef CET_FP8_SCALED
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a.q, cat8(b[0].q, b[1].q), c, 0, 0, 0, 127, 0,
-                                                            fp8_wscale());
-#else
     c = mfma8(a.q, b->lo, c);
     return mfma8(a.q, b->hi, c);
-#endif
   }
 }
 
@@ -253,13 +216,7 @@ struct Img : ImgBase<P> {
 #endif
     XF<P> r;
     if constexpr (P == P_FP8) {
-#ifdef CET_FP8_SCALED
-      const i32x2 a = *reinterpret_cast<const i32x2*>(base + row * RS + k0);
-      const i32x2 b = *reinterpret_cast<const i32x2*>(base + row * RS + k0 + 32);
-      r.q = i32x8{a[0], a[1], b[0], b[1], a[0], a[1], b[0], b[1]};
-#else
       r.q = *reinterpret_cast<const long*>(base + row * RS + k0);
-#endif
     } else {
       const int o = off(row, 2 * k0);
       r.h = *reinterpret_cast<const bf16x8*>(base + o);
@@ -373,12 +330,8 @@ __device__ __forceinline__ WF<P> wfrag(const Mem& m, uint32_t off, int lane) {
   WF<P> r;
   const uint4 v = wload16(m, off, lane);
   if constexpr (P == P_FP8) {
-#ifdef CET_FP8_SCALED
-    r.q = __builtin_bit_cast(i32x4, v);
-#else
     r.hi = (long)(((unsigned long long)v.y << 32) | v.x);
     r.lo = (long)(((unsigned long long)v.w << 32) | v.z);
-#endif
   } else {
     r.h = __builtin_bit_cast(bf16x8, v);
     if constexpr (P == P_X3) r.l = __builtin_bit_cast(bf16x8, wload16(m, off + m.wlo, lane));

@@ -37,6 +37,51 @@ def names(e_layers=(4,), d_layers=3):
 NAMES = names()
 
 
+def stragglers(sub, start, end, tot, clk):
+    """Where the last workgroups ran (slots 96 / 97: HW_ID and XCC_ID, gfx9 field layout): end-time tail,
+    per-XCC ends, workgroups per CU, and what the latest 5 % have in common."""
+    hw, xcc = sub[:, 96].astype(np.int64), sub[:, 97].astype(np.int64)
+    if not hw.any():
+        return
+    xcc = xcc & 0xF
+    cu = (hw >> 8) & 0xF
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 0x7
+    simd = (hw >> 4) & 3
+    key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    q = np.percentile(end, [50, 90, 99])
+    print(f"WG end tail: p50 {q[0]:.2f}  p90 {q[1]:.2f}  p99 {q[2]:.2f}  max {end.max():.2f} us")
+    for x in np.unique(xcc):
+        m = xcc == x
+        print(f"  XCC {x}: {m.sum()} WGs, {len(np.unique(key[m]))} CUs, end median {np.median(end[m]):.2f} max "
+              f"{end[m].max():.2f} us, clock median {np.median(clk[m]):.3f} GHz, WG cycles median {np.median(tot[m]):.0f}")
+    ukeys, counts = np.unique(key, return_counts=True)
+    hist = {int(c): int((counts == c).sum()) for c in np.unique(counts)}
+    print(f"  CUs used {len(ukeys)}; WGs per CU: {hist}")
+    per_cu = {k: c for k, c in zip(ukeys, counts)}
+    late = end >= np.percentile(end, 95)
+    wpc = np.array([per_cu[k] for k in key])
+    print(f"  latest 5 %: start offset mean {start[late].mean():.2f} us (all {start.mean():.2f}), WG cycles mean "
+          f"{tot[late].mean():.0f} (all {tot.mean():.0f}), clock mean {clk[late].mean():.3f} GHz (all {clk.mean():.3f}), "
+          f"WGs on their CU mean {wpc[late].mean():.2f} (all {wpc.mean():.2f}), first SIMD of wave 0: "
+          f"{np.bincount(simd[late], minlength=4).tolist()}")
+    # a CU's two workgroups: the later one's end against the earlier one's
+    bidx = np.arange(len(key))   # v4: every workgroup stamps its own row, so the row is the block index
+    two = [np.nonzero(key == k)[0] for k in ukeys if per_cu[k] == 2]
+    if two:
+        dif = np.array([bidx[i[1]] - bidx[i[0]] for i in two])
+        vals, cnts = np.unique(dif, return_counts=True)
+        first_low = np.mean([end[i[0]] <= end[i[1]] for i in two])
+        print(f"  CU pair block-index distance (top): " +
+              ", ".join(f"{v}: {c}" for v, c in sorted(zip(vals, cnts), key=lambda t: -t[1])[:4]) +
+              f";  the lower block index ends first in {100 * first_low:.0f} % of pairs")
+    pairs = [np.sort(end[key == k]) for k in ukeys if per_cu[k] == 2]
+    if pairs:
+        pe = np.array(pairs)
+        print(f"  CU pairs: first end median {np.median(pe[:, 0]):.2f}, second end median {np.median(pe[:, 1]):.2f}, "
+              f"gap median {np.median(pe[:, 1] - pe[:, 0]):.2f} p90 {np.percentile(pe[:, 1] - pe[:, 0], 90):.2f} us")
+
+
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     e43 = len(sys.argv) > 2 and sys.argv[2] == "e43"   # the TimingAnalysis stack (attn full, e_layers [4, 3])
@@ -81,6 +126,7 @@ def main():
         print(f"kernel span (first WG start -> last WG end): {span:.2f} us;  WG start offsets: median "
               f"{np.median(start):.2f} us, max {start.max():.2f} us;  WG end: median {np.median(end):.2f} us, "
               f"min {end.min():.2f} us;  in-kernel clock (memtime/realtime): median {np.median(clk):.3f} GHz")
+        stragglers(sub, start, end, tot, clk)
     SUBN = ["K/V projection", "Q projection", "phase A (M)", "top-u select", "phase C (softmax·V)", "phase D (rest)"]
     for c, base in ((0, 100), (1, 108)):
         ss = sub[:, base:base + 7]
