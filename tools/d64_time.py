@@ -2,7 +2,7 @@
 the fused layer-wise form) at batch B: back-to-back launches between two HIP events, and the output's
 checksum so builds can be compared for equality.
 
-    python tools/d64_time.py [B] [launches]      (GPU box; CET_LIB selects the build)
+    python tools/d64_time.py [B] [launches] [precision]      (GPU box; CET_LIB selects the build)
 """
 import os
 import sys
@@ -20,6 +20,8 @@ N = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 dev = torch.device("cuda:0")
 m, _ = informer(dev, [4, 3], "full", seq_len=25, d_model=64)
 eng = m.engine(dev)
+if len(sys.argv) > 3:   # e.g. "bf16": the bf16-operand instance of the fused form
+    eng.set_precision(sys.argv[3])
 g = torch.Generator().manual_seed(5)
 xe = torch.randn(B, 25, 16, generator=g).to(dev)
 xd = torch.randn(B, 15, 16, generator=g).to(dev)
