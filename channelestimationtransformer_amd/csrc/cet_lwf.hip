@@ -467,6 +467,103 @@ __device__ __forceinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, 
   }
 }
 
+// Attention for small heads without ProbSparse draws, in registers (the d_model-64 instance: E_ = 8, LQ and
+// LK ≤ 32).  Sᵀ = K·Qᵀ on v_mfma_f32_16x16x4_f32 with the keys as rows, so lane (g, c) holds query c's scores
+// against keys 4g .. 4g + 3 of each key tile; the softmax reduces over the lane's registers and the four
+// lane groups; Oᵀ = Vᵀ·Pᵀ takes those probabilities as its B operand unchanged (MFMA j's k index g is key
+// 4g + j of the tile), the E_ features padded to 16 rows.  fp32 throughout (fattn's arithmetic class); the
+// scores never touch LDS, so there is no scratch and no wave-local LDS synchronisation.
+// lane l's value of lane l ^ m through ds_bpermute: the compiler would turn a 16 / 32 xor shuffle into
+// v_permlane16/32_swap, which the ISA guard (tests/test_isa_guard.py) rejects inside a region whose EXEC the
+// structuriser may narrow
+__device__ __forceinline__ float bperm_xor(float v, int m) {
+  const int l = threadIdx.x & 63;
+  return __int_as_float(__builtin_amdgcn_ds_bpermute((l ^ m) << 2, __float_as_int(v)));
+}
+template <int E_, int NT>
+__device__ __forceinline__ void fattn_reg(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H,
+                                          int LQ, int LK, int causal, int mix, int AW) {
+  const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
+  AW = uni(AW);
+  Qo = uni(Qo); ldq = uni(ldq); Ko = uni(Ko); ldk = uni(ldk); Vo = uni(Vo); ldv = uni(ldv); Oo = uni(Oo);
+  ldo = uni(ldo); H = uni(H); LQ = uni(LQ); LK = uni(LK); causal = uni(causal); mix = uni(mix);
+  const float* Q = lsm + Qo;
+  const float* K = lsm + Ko;
+  const float* V = lsm + Vo;
+  float* O = lsm + Oo;
+  const int c = lane & 15, g = lane >> 4;
+  const int HE = H * E_;
+  const float scale = 1.0f / sqrtf((float)E_);
+  const int nkt = (LK + 15) >> 4, nqt = (LQ + 15) >> 4;
+  for (int h = w < AW ? w : H; h < H; h += AW) {
+    const int hc = h * E_;
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) {
+      if (qt >= nqt) break;
+      const int q = 16 * qt + c;
+      const int qr = q < LQ ? q : LQ - 1;   // padded query columns read a valid row (their output is dropped)
+      f32x4 st[NT];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt) {
+        st[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (kt < nkt) {
+          const int kr = 16 * kt + c < LK ? 16 * kt + c : LK - 1;
+#pragma unroll
+          for (int kk = 0; kk < E_; kk += 4)
+            st[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(K[kr * ldk + hc + kk + g], Q[qr * ldq + hc + kk + g], st[kt],
+                                                          0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = 16 * kt + 4 * g + r;
+            const bool off = key >= LK || (causal && key > q);
+            st[kt][r] = off ? -INFINITY : st[kt][r] * scale;
+            mx = fmaxf(mx, st[kt][r]);
+          }
+        }
+      }
+      mx = fmaxf(mx, bperm_xor(mx, 16));
+      mx = fmaxf(mx, bperm_xor(mx, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt)
+        if (kt < nkt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            st[kt][r] = expf(st[kt][r] - mx);   // masked keys: exp(−inf) = 0
+            sum += st[kt][r];
+          }
+      sum += bperm_xor(sum, 16);
+      sum += bperm_xor(sum, 32);
+      const float inv = 1.0f / sum;
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt)
+        if (kt < nkt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int key = 16 * kt + 4 * g + j;
+            const float v = c < E_ && key < LK ? V[key * ldv + hc + c] : 0.f;
+            o = __builtin_amdgcn_mfma_f32_16x16x4f32(v, st[kt][j], o, 0, 0, 0);
+          }
+      // lane (g, c): features 4g .. 4g + 3 of query c
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = 4 * g + r;
+        if (q < LQ && e < E_) {
+          const float y = o[r] * inv;
+          if (!mix) {
+            O[q * ldo + hc + e] = y;
+          } else {
+            const int f = h * LQ * E_ + q * E_ + e, row = f / HE;
+            O[row * ldo + (f - row * HE)] = y;
+          }
+        }
+      }
+    }
+  }
+}
+
 #ifdef LWF_STAMPS
 // diagnostic build: cycles of workgroup 0 per category (0 GEMM, 1 attention, 2 LayerNorm, 3 other), printed
 #define LWF_ST_DECL uint64_t st_acc[4] = {0, 0, 0, 0}; uint64_t st_prev = __builtin_amdgcn_s_memtime();
@@ -553,8 +650,11 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       const int call = ly->call;
       const int u = call >= 0 ? p->call_u[call] : L;
       const int sparse = p->prob && call >= 0 && u < L;
-      fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
-            u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
+      if (FIX && !sparse)
+        fattn_reg<8, 2>(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, L, L, 0, 0, AW);
+      else
+        fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
+              u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
     }
     __syncthreads();
     LWF_ST(1)
@@ -657,8 +757,11 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       const int call = ly->call;
       const int u = call >= 0 ? p->call_u[call] : Ld;
       const int sparse = p->prob && call >= 0 && u < Ld;
-      fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
-            call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
+      if (FIX && !sparse)
+        fattn_reg<8, 2>(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, Ld, Ld, 1, p->mix, AW);
+      else
+        fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
+              call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
     }
     __syncthreads();
     LWF_ST(1)
@@ -673,7 +776,10 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     fgemm<BF, 0, FIX ? 128 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
-    fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
+    if (FIX)
+      fattn_reg<8, 2>(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, Ld, S, 0, 0, AW);
+    else
+      fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
     __syncthreads();
     LWF_ST(1)
     fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
