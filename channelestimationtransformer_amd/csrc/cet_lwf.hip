@@ -78,12 +78,32 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // gout: rows t ≥ t0 go to gout[(t − t0)·ldo + n] in HBM instead of Y.  MT is compile-time, so the K loop is
 // straight-line code (no per-MFMA branch, so no wait on every outstanding load before each MFMA).  The A
 // reads of k ≥ K land in the padded, finite part of the LDS image and meet zero weights.
-template <bool BF, int AMODE, int MT, int NF = 0, int KF = 0>
+// The bf16 weight fragments of a wave's first n-tile of a compile-time-shaped GEMM, requested before the barrier
+// (and the phase) that precedes it, so the GEMM phase starts on its MFMAs (fgemm's task split: with two
+// m-tiles the wave's first n-tile is w mod 4, otherwise w).
+template <int KF>
+struct WBPre {
+  bf16x8 v[(KF + 31) / 32];
+};
+template <int NF, int KF>
+__device__ __forceinline__ WBPre<KF> fgemm_pre(const bf16x8* __restrict__ pwb, const FG g, int L) {
+  constexpr int KS = (KF + 31) / 32, NT = (NF + 15) / 16;
+  const int w = uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int n0 = ((uni(L) + 15) >> 4) == 2 ? w % (NW / 2) : w;
+  const int nt = n0 < NT ? n0 : 0;
+  const bf16x8* wp = pwb + g.wb + (size_t)nt * KS * 64 + lane;
+  WBPre<KF> p;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) p.v[ks] = wp[(size_t)ks * 64];
+  return p;
+}
+
+template <bool BF, int AMODE, int MT, int NF = 0, int KF = 0, class PreT = std::nullptr_t>
 __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const float* __restrict__ pw,
                                         const bf16x8* __restrict__ pwb, const FG g,
                                         int A, int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe,
                                         int act, int res, float* __restrict__ gout, int t0, int ldo, int m0, int n0,
-                                        int nstep) {
+                                        int nstep, const PreT& pre = nullptr) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, q4 = lane >> 4;
   const int N = NF ? NF : uni(g.N), K = KF ? KF : uni(g.K);   // NF / KF: the plan's N / K at compile time
@@ -139,8 +159,18 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
       const bf16x8* wp = pwb + g.wb + (size_t)nt * KS * 64 + lane;
       bf16x8 wv[KSP];
       if constexpr (KF) {
+        if constexpr (!std::is_same_v<PreT, std::nullptr_t>) {
+          if (nt == n0) {   // the fragments requested before the barrier (fgemm_pre)
 #pragma unroll
-        for (int ks = 0; ks < KSM; ++ks) wv[ks] = wp[(size_t)ks * 64];
+            for (int ks = 0; ks < KSM; ++ks) wv[ks] = pre.v[ks];
+          } else {
+#pragma unroll
+            for (int ks = 0; ks < KSM; ++ks) wv[ks] = wp[(size_t)ks * 64];
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < KSM; ++ks) wv[ks] = wp[(size_t)ks * 64];
+        }
       }
       f32x4 acc[MT];
 #pragma unroll
@@ -224,20 +254,21 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
 
 // The GEMM's task split over the eight waves (≤ 48 rows: the plan's validated range, cet_lw_host.cpp
 // build_fused): two m-tiles are split between the wave halves, one or three stay whole per wave.
-template <bool BF, int AMODE, int NF = 0, int KF = 0>
+template <bool BF, int AMODE, int NF = 0, int KF = 0, class PreT = std::nullptr_t>
 __device__ __forceinline__ void fgemm(const float* __restrict__ blob, const float* __restrict__ pw,
                                       const bf16x8* __restrict__ pwb, const FG g, int A,
                                       int lda, int Cin, int L, int Y, int ldy, const float* __restrict__ pe, int act,
-                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0) {
+                                      int res, float* __restrict__ gout = nullptr, int t0 = 0, int ldo = 0,
+                                      const PreT& pre = nullptr) {
   const int w = uni(threadIdx.x >> 6);
   A = uni(A); lda = uni(lda); Cin = uni(Cin); L = uni(L); Y = uni(Y); ldy = uni(ldy); act = uni(act); res = uni(res);
   switch ((L + 15) >> 4) {
-    case 1: fgemm_t<BF, AMODE, 1, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    case 1: fgemm_t<BF, AMODE, 1, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW, pre); break;
     case 2:
       fgemm_t<BF, AMODE, 1, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, w / (NW / 2), w % (NW / 2),
-                        NW / 2);
+                        NW / 2, pre);
       break;
-    default: fgemm_t<BF, AMODE, 3, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW); break;
+    default: fgemm_t<BF, AMODE, 3, NF, KF>(blob, pw, pwb, g, A, lda, Cin, L, Y, ldy, pe, act, res, gout, t0, ldo, 0, w, NW, pre); break;
   }
 }
 
@@ -637,6 +668,14 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     __syncthreads();
     LWF_ST(3)
   }
+  // the first n-tile's bf16 weight fragments of a GEMM, requested ahead of the barrier before it (the checkpoint
+  // instance with bf16 operands; nullptr elsewhere)
+  auto wpre = [&](auto NFc, auto KFc, const FG& gg, int Lr) __attribute__((always_inline)) {
+    if constexpr (FIX && BF)
+      return fgemm_pre<decltype(NFc)::value, decltype(KFc)::value>(pwb, gg, Lr);
+    else
+      return nullptr;
+  };
   // ---- encoders.  One encoder layer of rows L (a compile-time constant in the checkpoint instance, so its
   //      GEMM tile counts and attention bounds fold); returns the rows after its distil conv.
   auto enc_layer = [&](auto Lc, int i, int l) __attribute__((always_inline)) {
@@ -656,19 +695,25 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
         fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
               u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
     }
+    const auto po = wpre(ICn<64>{}, ICn<64>{}, ly->o, L);
     __syncthreads();
     LWF_ST(1)
-    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1);   // x + attention (encoder.py:44-49)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->o, CTX, ldH, 0, L, X, ldD, nullptr, 0, 1, nullptr, 0, 0,
+                                             po);   // x + attention (encoder.py:44-49)
+    const auto pf1 = wpre(ICn<64>{}, ICn<64>{}, ly->f1, L);
     const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
     __syncthreads();
     LWF_ST(0)
     fln<NC>(X, ldD, L, D, n1, X, ldD);
     __syncthreads();
     LWF_ST(2)
-    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0);
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f1, X, ldD, 0, L, T, ldF, nullptr, p->act, 0, nullptr, 0,
+                                             0, pf1);
+    const auto pf2 = wpre(ICn<64>{}, ICn<64>{}, ly->f2, L);
     __syncthreads();
     LWF_ST(0)
-    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1);
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f2, T, ldF, 0, L, X, ldD, nullptr, 0, 1, nullptr, 0, 0,
+                                             pf2);
     const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
     __syncthreads();
     LWF_ST(0)
@@ -763,9 +808,11 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
         fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
               call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
     }
+    const auto pdo = wpre(ICn<64>{}, ICn<64>{}, ly->o, Ld);
     __syncthreads();
     LWF_ST(1)
-    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm1(x + self-attention)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->o, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0,
+                                             pdo);   // norm1(x + self-attention)
     const LnPre<NC> n1 = lnpre<NC>(blob + ly->g1, blob + ly->b1, D);
     __syncthreads();
     LWF_ST(0)
@@ -780,9 +827,11 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       fattn_reg<8, 2>(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, Ld, S, 0, 0, AW);
     else
       fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
+    const auto pco = wpre(ICn<64>{}, ICn<64>{}, ly->co, Ld);
     __syncthreads();
     LWF_ST(1)
-    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm2(x + cross-attention)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->co, CTX, ldH, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0,
+                                             pco);   // norm2(x + cross-attention)
     const LnPre<NC> n2 = lnpre<NC>(blob + ly->g2, blob + ly->b2, D);
     __syncthreads();
     LWF_ST(0)
@@ -790,9 +839,11 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     __syncthreads();
     LWF_ST(2)
     fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f1, XD, ldD, 0, Ld, T, ldF, nullptr, p->act, 0);
+    const auto pdf2 = wpre(ICn<64>{}, ICn<64>{}, ly->f2, Ld);
     __syncthreads();
     LWF_ST(0)
-    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1);   // norm3(x + y)
+    fgemm<BF, 0, FIX ? 64 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->f2, T, ldF, 0, Ld, XD, ldD, nullptr, 0, 1, nullptr, 0, 0,
+                                             pdf2);   // norm3(x + y)
     const LnPre<NC> n3 = lnpre<NC>(blob + ly->g3, blob + ly->b3, D);
     __syncthreads();
     LWF_ST(0)
