@@ -498,12 +498,6 @@ __device__ __forceinline__ void fattn(int Qo, int ldq, int Ko, int ldk, int Vo, 
   }
 }
 
-// Attention for small heads without ProbSparse draws, in registers (the d_model-64 instance: E_ = 8, LQ and
-// LK ≤ 32).  Sᵀ = K·Qᵀ on v_mfma_f32_16x16x4_f32 with the keys as rows, so lane (g, c) holds query c's scores
-// against keys 4g .. 4g + 3 of each key tile; the softmax reduces over the lane's registers and the four
-// lane groups; Oᵀ = Vᵀ·Pᵀ takes those probabilities as its B operand unchanged (MFMA j's k index g is key
-// 4g + j of the tile), the E_ features padded to 16 rows.  fp32 throughout (fattn's arithmetic class); the
-// scores never touch LDS, so there is no scratch and no wave-local LDS synchronisation.
 // lane l's value of lane l ^ m through ds_bpermute: the compiler would turn a 16 / 32 xor shuffle into
 // v_permlane16/32_swap, which the ISA guard (tests/test_isa_guard.py) rejects inside a region whose EXEC the
 // structuriser may narrow
@@ -511,13 +505,20 @@ __device__ __forceinline__ float bperm_xor(float v, int m) {
   const int l = threadIdx.x & 63;
   return __int_as_float(__builtin_amdgcn_ds_bpermute((l ^ m) << 2, __float_as_int(v)));
 }
-template <int E_, int NT>
+// Attention for small heads without ProbSparse draws, in registers: E ≤ EM features per head (a multiple of
+// 4), LQ and LK ≤ 16·NT — the d_model-64 checkpoint instance (E = 8) and any plan of the runtime-shape instance
+// within those bounds (EM = 16, NT = 2).  Sᵀ = K·Qᵀ on v_mfma_f32_16x16x4_f32 with the keys as rows, so lane
+// (g, c) holds query c's scores against keys 4g .. 4g + 3 of each key tile; the softmax reduces over the lane's
+// registers and the four lane groups; Oᵀ = Vᵀ·Pᵀ takes those probabilities as its B operand unchanged (MFMA
+// j's k index g is key 4g + j of the tile), the E features padded to 16 rows.  fp32 throughout (fattn's
+// arithmetic class); the scores never touch LDS, so there is no scratch and no wave-local LDS synchronisation.
+template <int EM, int NT>
 __device__ __forceinline__ void fattn_reg(int Qo, int ldq, int Ko, int ldk, int Vo, int ldv, int Oo, int ldo, int H,
-                                          int LQ, int LK, int causal, int mix, int AW) {
+                                          int E_, int LQ, int LK, int causal, int mix, int AW) {
   const int lane = threadIdx.x & 63, w = uni(threadIdx.x >> 6);
   AW = uni(AW);
   Qo = uni(Qo); ldq = uni(ldq); Ko = uni(Ko); ldk = uni(ldk); Vo = uni(Vo); ldv = uni(ldv); Oo = uni(Oo);
-  ldo = uni(ldo); H = uni(H); LQ = uni(LQ); LK = uni(LK); causal = uni(causal); mix = uni(mix);
+  ldo = uni(ldo); H = uni(H); E_ = uni(E_); LQ = uni(LQ); LK = uni(LK); causal = uni(causal); mix = uni(mix);
   const float* Q = lsm + Qo;
   const float* K = lsm + Ko;
   const float* V = lsm + Vo;
@@ -541,9 +542,10 @@ __device__ __forceinline__ void fattn_reg(int Qo, int ldq, int Ko, int ldk, int 
         if (kt < nkt) {
           const int kr = 16 * kt + c < LK ? 16 * kt + c : LK - 1;
 #pragma unroll
-          for (int kk = 0; kk < E_; kk += 4)
-            st[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(K[kr * ldk + hc + kk + g], Q[qr * ldq + hc + kk + g], st[kt],
-                                                          0, 0, 0);
+          for (int kk = 0; kk < EM; kk += 4)
+            if (kk < E_)
+              st[kt] = __builtin_amdgcn_mfma_f32_16x16x4f32(K[kr * ldk + hc + kk + g], Q[qr * ldq + hc + kk + g],
+                                                            st[kt], 0, 0, 0);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = 16 * kt + 4 * g + r;
@@ -638,6 +640,8 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
   // LDS regions (float offsets into lsm)
   const int E1 = PV(oE1), X = PV(oX), T = PV(oT), CTX = PV(oCTX), ENC = PV(oENC), XD = PV(oXD);
   const int AW = PV(attn_waves);
+  // heads the register attention (fattn_reg) carries: at most 16 features, a multiple of 4
+  const bool reg_heads = E <= 16 && (E & 3) == 0;
   const int scr = PV(oSCR) + (w < AW ? w : 0) * PV(scr_floats);
   // zero LDS (padded rows and columns stay finite: they only ever meet zero weights or masked keys), then
   // stage this sequence's encoder input rows
@@ -689,8 +693,8 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       const int call = ly->call;
       const int u = call >= 0 ? p->call_u[call] : L;
       const int sparse = p->prob && call >= 0 && u < L;
-      if (FIX && !sparse)
-        fattn_reg<8, 2>(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, L, L, 0, 0, AW);
+      if (!sparse && (FIX || (reg_heads && L <= 32)))
+        fattn_reg<FIX ? 8 : 16, 2>(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, AW);
       else
         fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, L, L, 0, 0, sparse, call >= 0 ? p->call_U[call] : 0,
               u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
@@ -802,8 +806,8 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
       const int call = ly->call;
       const int u = call >= 0 ? p->call_u[call] : Ld;
       const int sparse = p->prob && call >= 0 && u < Ld;
-      if (FIX && !sparse)
-        fattn_reg<8, 2>(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, Ld, Ld, 1, p->mix, AW);
+      if (!sparse && (FIX || (reg_heads && Ld <= 32)))
+        fattn_reg<FIX ? 8 : 16, 2>(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, AW);
       else
         fattn(T, ldT, T + HE, ldT, T + 2 * HE, ldT, CTX, ldH, H, E, Ld, Ld, 1, p->mix, sparse,
               call >= 0 ? p->call_U[call] : 0, u, call >= 0 ? idx + p->call_off[call] : nullptr, scr, AW);
@@ -823,8 +827,8 @@ __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(4))) l
     fgemm<BF, 0, FIX ? 128 : 0, FIX ? 64 : 0>(blob, pw, pwb, ly->ckv, ENC, ldD, 0, S, KV, ldKV, nullptr, 0, 0);
     __syncthreads();
     LWF_ST(0)
-    if (FIX)
-      fattn_reg<8, 2>(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, Ld, S, 0, 0, AW);
+    if (FIX || (reg_heads && Ld <= 32 && S <= 32))
+      fattn_reg<FIX ? 8 : 16, 2>(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, AW);
     else
       fattn(QC, ldH, KV, ldKV, KV + HE, ldKV, CTX, ldH, H, E, Ld, S, 0, 0, 0, 0, Ld, nullptr, scr, AW);
     const auto pco = wpre(ICn<64>{}, ICn<64>{}, ly->co, Ld);
