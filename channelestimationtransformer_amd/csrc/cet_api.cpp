@@ -1425,10 +1425,16 @@ static bool encoder_rows_are(const InformerPlan& p, int e, int n, const int* lin
   }
   return true;
 }
-static int plan_shape(const InformerPlan& p) {
+// CET_LDS_POISON=1: the v4 kernels fill their LDS with NaN at entry (diagnostic, tests/test_gpu_poison.py)
+static int lds_poison_requested() {
+  const char* v = std::getenv("CET_LDS_POISON");
+  return v && std::strcmp(v, "0") != 0 ? 1 : 0;
+}
+static int plan_shape(const InformerPlan& p, int dff) {
   static const int lin4[4] = {90, 45, 23, 12}, lout4[4] = {45, 23, 12, 12};
   static const int lin3[3] = {45, 23, 12}, lout3[3] = {23, 12, 12};
-  if (p.seq_len != 90) return V4S_GENERIC;
+  // the compile-time instances exist for d_ff 64 only: any other d_ff keeps the generic (and generic split) ones
+  if (p.seq_len != 90 || dff != 64) return V4S_GENERIC;
   if (p.n_enc == 1 && encoder_rows_are(p, 0, 4, lin4, lout4)) return V4S_C2;
   if (p.n_enc == 2 && encoder_rows_are(p, 0, 4, lin4, lout4) && encoder_rows_are(p, 1, 3, lin3, lout3) && p.S == 24 &&
       p.dec_len <= 16)
@@ -1441,9 +1447,10 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   InformerArgs b = a;
   b.wlo = (uint32_t)(e->wblob.size() * 2);
   const char* c2env = std::getenv("CET_V4_C2");   // "0": the generic instance for every plan (A/B)
-  b.shape = c2env && std::strcmp(c2env, "0") == 0 ? V4S_GENERIC : plan_shape(p);
+  b.shape = c2env && std::strcmp(c2env, "0") == 0 ? V4S_GENERIC : plan_shape(p, e->icfg.d_ff);
   b.stagger = 0;
   if (const char* sg = std::getenv("CET_STAGGER")) b.stagger = std::atoi(sg);
+  b.poison = lds_poison_requested();
   b.enc_split = 0;
   b.enc_xchg = nullptr;
   b.enc_count = nullptr;
@@ -1505,6 +1512,10 @@ static int forward_lw(cet_engine* e, const float* x_enc, const float* x_dec, int
     any_idx = any_idx || e->idx_set[c];
   }
   if (any_idx && !explicit_idx) return fail(CET_E_STATE, "ProbSparse indices set for some calls only");
+  // refused before any draw or timing event, so a refused forward leaves the RNG stream and the timing slots alone
+  if (e->lw->bf16_refused(attns))
+    return fail(CET_E_INVALID, "bf16 operands need the fused layer-wise form (no attention maps, a working set that "
+                               "fits one workgroup, feature counts that are multiples of 8)");
   if (n_calls && !explicit_idx && !e->native_rng)
     return fail(CET_E_STATE, "ProbSparse indices not set (cet_set_prob_indices for every call, or cet_seed)");
   if (n_calls) {
@@ -1534,9 +1545,6 @@ static int forward_lw(cet_engine* e, const float* x_enc, const float* x_dec, int
   }
   const int tk = timing_mark(e, st);
   const int rc = e->lw->forward(x_enc, x_dec, B, out, attns, e->lw->d_idx, st);
-  if (rc == -7)
-    return fail(CET_E_INVALID, "bf16 operands need the fused layer-wise form (no attention maps, a working set that "
-                               "fits one workgroup, feature counts that are multiples of 8)");
   if (tk >= 0) (void)hipEventRecord(e->t_ev[2 * tk + 1], st);
   e->last_path = e->lw->last_fused ? CET_PATH_LW_FUSED : CET_PATH_LW;
   e->last_kernel = !e->lw->last_fused ? ""   // the operator path launches several kernels
@@ -1578,6 +1586,7 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     a.out = out;
     a.dbg = e->dbg;
     a.B = B;
+    a.poison = lds_poison_requested();
     const char* c3env = std::getenv("CET_V4_C3");
     a.c3 = e->tp.src_len == 90 && e->tp.tgt_len == 15 && !(c3env && std::strcmp(c3env, "0") == 0);
     {
@@ -1647,6 +1656,10 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     any_idx = any_idx || e->idx_set[c];
   }
   if (any_idx && !explicit_idx) return fail(CET_E_STATE, "ProbSparse indices set for some calls only");
+  // refused before any draw or timing event, so a refused forward leaves the RNG stream and the timing slots alone
+  if (e->lw->bf16_refused(attns))
+    return fail(CET_E_INVALID, "bf16 operands need the fused layer-wise form (no attention maps, a working set that "
+                               "fits one workgroup, feature counts that are multiples of 8)");
   if (p.n_calls && !explicit_idx && !e->native_rng)
     return fail(CET_E_STATE, "ProbSparse indices not set (cet_set_prob_indices for every call, or cet_seed)");
   if (e->native_rng && p.n_calls && !e->host_sampler && !explicit_idx) {

@@ -34,6 +34,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   const int b = SPLIT ? (int)blockIdx.x / nsplit : (int)blockIdx.x;
   const int my_e = SPLIT ? (int)blockIdx.x - b * nsplit : -1;   // the one encoder of this workgroup
   if (b >= a.B) return;
+  if (a.poison) lds_poison<NTHREADS>(lds, a.lds_bytes);
   const int w = wave_id();
 #ifdef CET_STAGGER
   // experiment: CET_STAGGER = mask·65536 + units: workgroups with (b & mask) != 0 idle units·64 cycles first
@@ -101,7 +102,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   constexpr bool PRE = false;
 #endif
   f32x4 t0a = {0.f, 0.f, 0.f, 0.f}, t0b = t0a;
-  int t0n = 0;   // 16-byte pieces of call 0's table (≤ 96 rows × 96 B = 576)
+  int t0n = 0;   // 16-byte pieces of call 0's table (≤ 96 rows × 104 B / 16 = 624: two per thread)
+  static_assert(LMAX * CNT_STRIDE / 16 <= 2 * NTHREADS, "call 0's table staged with two f32x4 per thread");
   if constexpr (PRE) {
     const int c0 = PL.enc[PL.enc_first[0]].call;
     if (a.cnt && c0 >= 0 && PL.calls[c0].u < PL.calls[c0].LQ) {

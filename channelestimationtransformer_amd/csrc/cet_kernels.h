@@ -42,6 +42,7 @@ struct InformerArgs {
                               // cycles at entry (-DCET_STAGGER builds only)
   int shape;                  // v4_shape of the plan (V4S_*): the bf16 production launch takes the instance with its
                               // encoder rows as compile-time constants
+  int poison;                 // diagnostic (CET_LDS_POISON=1): every LDS byte NaN at entry, before anything is staged
 };
 
 // Plans with a compile-time instance (cet_api.cpp plan_shape): C2's encoder (one encoder, rows 90 → 45 → 23 → 12,
@@ -102,6 +103,8 @@ struct TransformerArgs {
   int B;
   int c3;   // the plan is C3's (src_len 90, tgt_len 15): the production launch takes the instance with those
             // lengths at compile time
+  int poison;      // diagnostic (CET_LDS_POISON=1): every LDS byte NaN at entry
+  int lds_bytes;   // dynamic LDS of the launch (set by the launcher)
 };
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize, 160 KiB) for `kern` on the CURRENT device,

@@ -180,6 +180,9 @@ struct Model {
   // bf16 GEMM operands (cet_set_precision "bf16" on a layer-wise engine): the fused form only, for feature
   // counts that are multiples of 8 (a lane's 8 consecutive k never straddle a conv tap)
   bool bf16 = false, fused_bf_ok = false;
+  // whether a forward with (or without) attention maps runs the fused form, and whether bf16 can run it
+  bool will_fuse(const float* attns) const { return fused_ok && use_fused && !(attns && out_attn); }
+  bool bf16_refused(const float* attns) const { return bf16 && !(will_fuse(attns) && fused_bf_ok); }
   std::vector<float> pblob;
   std::vector<uint16_t> pbblob;   // Wb[nt][ks][lane][j] = bf16(W[16nt + (lane & 15)][32ks + 8(lane >> 4) + j])
   FPlan* d_fplan = nullptr;

@@ -128,8 +128,9 @@ int Model::build_fused() {
           }
     const int KS = (K + 31) / 32;
     const size_t atb = pbblob.size();
-    pbblob.resize(atb + (size_t)NT * KS * 512, 0);
-    for (int nt = 0; nt < NT; ++nt)
+    // the bf16 fragments only for a bf16 engine (the precision is fixed when the model is planned)
+    if (bf16) pbblob.resize(atb + (size_t)NT * KS * 512, 0);
+    for (int nt = 0; bf16 && nt < NT; ++nt)
       for (int ks = 0; ks < KS; ++ks)
         for (int lane = 0; lane < 64; ++lane)
           for (int j = 0; j < 8; ++j) {
@@ -184,8 +185,11 @@ int Model::build_fused() {
   if (hipMemcpy(d_pblob, pblob.data(), pblob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return -1;
   if (d_pbblob) (void)hipFree(d_pbblob);
   d_pbblob = nullptr;
-  if (hipMalloc((void**)&d_pbblob, pbblob.size() * sizeof(uint16_t)) != hipSuccess) return -1;
-  if (hipMemcpy(d_pbblob, pbblob.data(), pbblob.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) return -1;
+  if (!pbblob.empty()) {
+    if (hipMalloc((void**)&d_pbblob, pbblob.size() * sizeof(uint16_t)) != hipSuccess) return -1;
+    if (hipMemcpy(d_pbblob, pbblob.data(), pbblob.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess)
+      return -1;
+  }
   fused_bf_ok = C % 8 == 0 && Cd % 8 == 0 && D % 8 == 0 && HE % 8 == 0 && dff % 8 == 0;
   if (hipMemcpy(d_fplan, &p, sizeof(FPlan), hipMemcpyHostToDevice) != hipSuccess) return -1;
   const char* fenv = std::getenv("CET_LW_FUSED_FIX");
@@ -244,7 +248,7 @@ static int capture(hipStream_t cap, hipGraphExec_t* exec, const std::function<in
 int Model::forward(const float* x_enc, const float* x_dec, int B, float* out, float* attns, const int32_t* idx_dev,
                    hipStream_t st) {
   // the fused form: one launch, no workspace, no staging copies
-  last_fused = fused_ok && use_fused && !(attns && out_attn);
+  last_fused = will_fuse(attns);
   if (bf16 && !(last_fused && fused_bf_ok)) return -7;   // bf16 operands exist in the fused form only
   if (last_fused)
     return launch_fused(d_fplan, D, fused_fix, bf16, fused_lds, d_blob, d_pblob, d_pbblob, x_enc, x_dec, out, idx_dev,

@@ -150,7 +150,9 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
     // weights.
     // compile-time K: every fragment of the n-tile requested up front; runtime K: one per step
     const int KS = (K + 31) >> 5;
-    constexpr int KSM = KF ? (KF + 31) / 32 : 8;   // K ≤ 256
+    // compile-time K: all KSM k-steps in one unrolled pass; runtime K: passes of 8 unrolled k-steps until
+    // every one of the KS steps is done (any K: the distil conv's 3·D, the embedding's 3·C, FFN2's d_ff)
+    constexpr int KSM = KF ? (KF + 31) / 32 : 8;
     constexpr int KSP = KF ? KSM : 1;
     for (int nt = n0; nt < NT; nt += nstep) {
       const int n = 16 * nt + r16;
@@ -175,10 +177,12 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks0 = 0; ks0 < (KF ? KSM : KS); ks0 += KSM) {
 #pragma unroll
-      for (int ks = 0; ks < KSM; ++ks) {
+      for (int j = 0; j < KSM; ++j) {
+        const int ks = ks0 + j;
         if (ks < KS) {
-          const bf16x8 w8 = KF ? wv[KF ? ks : 0] : wp[(size_t)ks * 64];
+          const bf16x8 w8 = KF ? wv[KF ? j : 0] : wp[(size_t)ks * 64];
           const int k = 32 * ks + 8 * q4;
           int tap = 0, c = k;
           if (AMODE) {
@@ -192,6 +196,7 @@ __device__ __forceinline__ void fgemm_t(const float* __restrict__ blob, const fl
             acc[m] = mfma16x16x32(cvt8(lo, hi), w8, acc[m]);
           }
         }
+      }
       }
       if (n >= N) continue;
 #pragma unroll

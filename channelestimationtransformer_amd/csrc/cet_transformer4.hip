@@ -31,6 +31,7 @@ __global__ void __launch_bounds__(NTHREADS, 4)
   const Mem M{make_rsrc(a.weights), make_rsrc(a.params), 0u};
   const int b = blockIdx.x;
   if (b >= a.B) return;
+  if (a.poison) lds_poison<NTHREADS>(lds, a.lds_bytes);
   const int w = wave_id();
   const float eps = 1e-6f;   // added to the unbiased std (buildingblocks.py:23-30)
 
@@ -220,6 +221,8 @@ extern "C" int cet_launch_transformer_v4(const cet::TransformerArgs* a, int dff,
   else if (dff == 128) kern = diag ? v4::transformer_forward_v4<128, true> : v4::transformer_forward_v4<128, false>;
   else return -3;
   if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
-  hipLaunchKernelGGL(kern, dim3(a->B), dim3(v4::NTHREADS), lds_bytes, stream, *a, a->plan);
+  cet::TransformerArgs args = *a;
+  args.lds_bytes = lds_bytes;
+  hipLaunchKernelGGL(kern, dim3(a->B), dim3(v4::NTHREADS), lds_bytes, stream, args, a->plan);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -322,6 +322,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
 }
 __device__ __forceinline__ uint4 wload16(const Mem& m, uint32_t off, int lane) {
+#ifdef CET_ABL_WL1
+  off &= 0x3C00u;   // ablation (wrong results): every weight tile from one L1-resident 16 KiB window
+#endif
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(m.w, lane * 16, (int)off, 0));
 }
 // this lane's fragment of the 1 KiB wave tile at uniform byte offset `off`
@@ -339,6 +342,9 @@ __device__ __forceinline__ WF<P> wfrag(const Mem& m, uint32_t off, int lane) {
   return r;
 }
 __device__ __forceinline__ f32x4 pload4(const Mem& m, uint32_t so, int vo) {
+#ifdef CET_ABL_PL1
+  so &= 0xFFu;   // ablation (wrong results): parameter vectors from one L1-resident window
+#endif
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(m.p, vo * 4, (int)(so * 4u), 0));
 }
 __device__ __forceinline__ float pload1(const Mem& m, uint32_t so, int vo) {
@@ -625,6 +631,23 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   const int nb = 16 * w + 4 * g;
   float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
   const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
+#ifdef CET_ABL_LN
+  // ablation (wrong results): no row statistics, no barriers — the LayerNorm's own cost, measured by its absence
+  (void)part; (void)stats; (void)eps; (void)unbiased_std;
+#pragma unroll
+  for (int mt = 0; mt < N; ++mt) {
+    if (mt < nmt) {
+      const int m = mt * 16 + c;
+      const f32x4 y = X.v[mt] * g0 + b0;
+      if (INPLACE) X.v[mt] = y;
+      if (m < rows) {
+        out.st4(m, nb, y);
+        if (out2) out2->st4(m, nb, y);
+      }
+    }
+  }
+  return;
+#endif
 #ifndef CET_LN_TWOPASS
   ln_publish(X, nmt, part);
   __syncthreads();
@@ -823,6 +846,15 @@ __device__ __forceinline__ void maxpool_eo(const Res<NIN>& in, int L, Res<MT>& o
 
 template <int N>
 using IC = std::integral_constant<int, N>;
+
+// Diagnostic (CET_LDS_POISON=1): every byte of the workgroup's dynamic LDS set to 0xFF — NaN as fp32, bf16 and
+// e4m3 — before the kernel stages or zeroes anything, so a read of a byte nothing wrote in this launch is a
+// deterministic NaN in the output instead of whatever the CU's previous workgroup left there.
+template <int NT>
+__device__ __forceinline__ void lds_poison(char* lds, int bytes) {
+  for (int i = tid_op(); i < bytes / 16; i += NT) reinterpret_cast<uint4*>(lds)[i] = uint4{~0u, ~0u, ~0u, ~0u};
+  __syncthreads();
+}
 
 __device__ __forceinline__ void stage(const float* __restrict__ src, float* dst, int L, int C, int CS) {
   for (int i = tid_op(); i < L * C; i += NTHREADS) {

@@ -455,6 +455,37 @@ def test_encoder_split_deeper_stacks_vs_oracle(e_layers, B):
     assert rel_nmse(out[rows], ref) < TOL
 
 
+def test_encoder_split_e43_rows_with_dff128_vs_oracle():
+    """The TimingAnalysis stack's rows (e_layers [4, 3], seq_len 90, attn "full") with d_ff 128: the
+    compile-time E43 instance exists for d_ff 64 only, so this plan must take the generic encoder-split
+    instance (it once got no instance at all and the forward failed).  B = 64 (split) and
+    B = 300 (B·n_enc > 512: the whole-sequence generic instance), against the float64 oracle."""
+    _gpu()
+    from channelestimationtransformer_amd.dataset import make_batch
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+    from oracle.informer_np import InformerConfig, InformerOracle
+
+    dev = torch.device("cuda:0")
+    m = InformerStack(16, 16, 16, 90, 10, 5, 5, 128, 8, [4, 3], 3, 128, 0.05, "full", "fixed", "gelu", False,
+                      True, dev)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(m._schema(), 8).items()})
+    m.eval()
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    orc = InformerOracle(InformerConfig(e_layers=(4, 3), d_ff=128, attn="full"), state)
+    for B, kernel in ((64, "cet::v4::informer_forward_v4<128, false, 0, true, 0, false>"),
+                      (300, "cet::v4::informer_forward_v4<128, false, 0, false, 0, false>")):
+        xe, xd, _ = make_batch(B, seed=500 + B)
+        with torch.no_grad():
+            res = m(torch.from_numpy(xe).to(dev), range(90), torch.from_numpy(xd).to(dev), range(15))
+        out = (res[0] if isinstance(res, tuple) else res).cpu().numpy()
+        assert m.engine(dev).last_kernel() == kernel
+        rows = np.r_[0:8, B - 8:B]
+        ref, _ = orc.forward(xe[rows], xd[rows], ())
+        assert np.isfinite(out).all()
+        assert rel_nmse(out[rows], ref) < TOL
+
+
 def test_attention_maps_materialised():
     _gpu()
     from engine_util import model_for, run_engine

@@ -403,3 +403,39 @@ def test_fused_layerwise_bf16_runtime_shapes_and_refusals():
         run_engine(m, xe, xd, idx, attns=True)
     with pytest.raises(Exception):
         eng.set_precision("split-bf16")
+
+
+def test_fused_layerwise_bf16_deep_k_vs_oracle():
+    """bf16 operands on the runtime-shape fused layer-wise instance with GEMMs deeper than 256: d_model 128
+    with a distil conv (K = 3·128 = 384) and d_ff 320 (FFN2 K = 320).  The runtime-K bf16 loop runs every
+    32-feature k-step of these (it once stopped after 8).  Seeded synthetic weights, attn "full"
+    (no selection flips under bf16), against the float64 oracle within the north star's 1e-4 and above the
+    fp32 bar, so the bf16 instance is what ran."""
+    _gpu()
+    from channelestimationtransformer_amd.dataset import make_batch
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+    from oracle.informer_np import InformerConfig, InformerOracle
+
+    dev = torch.device("cuda:0")
+    seq_len = 32
+    m = InformerStack(16, 16, 16, seq_len, 10, 5, 5, 128, 4, [2], 1, 320, 0.05, "full", "fixed", "gelu", False,
+                      True, dev)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(m._schema(), 6).items()})
+    m.eval()
+    state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    orc = InformerOracle(InformerConfig(seq_len=seq_len, d_model=128, n_heads=4, e_layers=(2,), d_layers=1,
+                                        d_ff=320, attn="full"), state)
+    eng = m.engine(dev)
+    eng.set_precision("bf16")
+    B = 19
+    xe, xd, _ = make_batch(B, seed=43)
+    xe = np.ascontiguousarray(xe[:, -seq_len:])
+    with torch.no_grad():
+        res = m(torch.from_numpy(xe).to(dev), range(seq_len), torch.from_numpy(xd).to(dev), range(15))
+    out = (res[0] if isinstance(res, tuple) else res).cpu().numpy()
+    assert eng.last_path() == "layerwise-fused"
+    assert eng.last_kernel() == "cet::lw::lw_fused (bf16 operands)"
+    ref, _ = orc.forward(xe, xd, ())
+    err = rel_nmse(out, ref)
+    assert TOL < err < BF16_TOL, err
