@@ -1656,10 +1656,6 @@ static int forward_impl(cet_engine* e, const float* x_enc, const float* x_dec, i
     any_idx = any_idx || e->idx_set[c];
   }
   if (any_idx && !explicit_idx) return fail(CET_E_STATE, "ProbSparse indices set for some calls only");
-  // refused before any draw or timing event, so a refused forward leaves the RNG stream and the timing slots alone
-  if (e->lw->bf16_refused(attns))
-    return fail(CET_E_INVALID, "bf16 operands need the fused layer-wise form (no attention maps, a working set that "
-                               "fits one workgroup, feature counts that are multiples of 8)");
   if (p.n_calls && !explicit_idx && !e->native_rng)
     return fail(CET_E_STATE, "ProbSparse indices not set (cet_set_prob_indices for every call, or cet_seed)");
   if (e->native_rng && p.n_calls && !e->host_sampler && !explicit_idx) {

@@ -336,7 +336,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       FINE(l, 0);
       static_assert(DFF / 16 <= NW, "FFN hidden n-tiles: at most one per wave");
       const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, ELD.f1, DFF / 16);   // conv1 (k=1) + activation
-      ln_res(X, nmt, L, M, ELD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      ln_res(X, nmt, L, M, ELD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr,
+             ST && stamps && e == 0 && l == 0 ? stamps + 32 : nullptr);   // L0 LN1 per-wave stamps: slots 32..63
       __syncthreads();
       STAMP();  // out-projection + LN1
       {
@@ -355,7 +356,8 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       FINE(l, 3);
       const int has_conv = ELD.conv.n;
       const bool last_of_stack = e == PL.n_enc - 1 && l == PL.enc_layers[e] - 1;
-      ln_res(X, nmt, L, M, ELD.ln2, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      ln_res(X, nmt, L, M, ELD.ln2, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr,
+             ST && stamps && e == 0 && l == 0 ? stamps + 64 : nullptr);   // L0 LN2: slots 64..95
       __syncthreads();
       STAMP();  // FFN + LN2
       if (dbg && ELD.dbg_layer >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_layer);

@@ -624,12 +624,19 @@ __device__ __forceinline__ void ln_apply_own(Res<N>& X, int nmt, int rows, f32x4
 // Two workgroup barriers inside; the caller adds one before the image is read.
 // INPLACE = false (pre-LN residual blocks, models/Transformer buildingblocks.py:214-226): the
 // normalised rows only go to the image(s); X keeps the residual.
+// lst (diagnostics, the C2 + stamps build): per-wave s_memtime at entry, after each barrier and at exit, in
+// lst[4·w + 0..3] — which part of a LayerNorm phase is the wave's own work and which is waiting for the others.
 template <int N, class Out, class Out2, bool INPLACE = true>
 __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
-                                       bool unbiased_std, float* part, const Out& out, const Out2* out2) {
+                                       bool unbiased_std, float* part, const Out& out, const Out2* out2,
+                                       unsigned long long* lst = nullptr) {
   const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
   const int nb = 16 * w + 4 * g;
   float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
+  auto LST = [&](int k) __attribute__((always_inline)) {
+    if (lst && lane == 0) lst[4 * w + k] = __builtin_amdgcn_s_memtime();
+  };
+  LST(0);
   const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
 #ifdef CET_ABL_LN
   // ablation (wrong results): no row statistics, no barriers — the LayerNorm's own cost, measured by its absence
@@ -651,6 +658,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
 #ifndef CET_LN_TWOPASS
   ln_publish(X, nmt, part);
   __syncthreads();
+  LST(1);
   auto row_stats = [&](int m) __attribute__((always_inline)) { return ln_row_stats(part, m, eps, unbiased_std); };
 #ifndef CET_LN_TWO_BARRIER
 #ifndef CET_LN_ONE_MAX
@@ -662,6 +670,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     // For the encoder's 3-6 tiles the redundant combining costs more than the barrier it saves
     // (-DCET_LN_ONE_MAX=3 ±0, =6 +1.2 us; profiles/r04/ab9/ab.log)
     ln_apply_own<N, Out, Out2, INPLACE>(X, nmt, rows, g0, b0, eps, unbiased_std, part, out, out2);
+    LST(3);
     return;
   }
 #endif
@@ -703,6 +712,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
   }
 #endif
   __syncthreads();
+  LST(2);
 #pragma unroll
   for (int mt = 0; mt < N; ++mt) {
     if (mt < nmt) {
@@ -716,6 +726,7 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
       }
     }
   }
+  LST(3);
 }
 
 // Two torch.nn.LayerNorms under one barrier, both in the own-rows form: the fused decoder layer 0's LN1

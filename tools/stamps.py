@@ -142,6 +142,24 @@ def main():
                "barrier", "store_xb+barrier"]
         dd = np.diff(pts, axis=1).mean(axis=0)
         print("L0 fine: " + "  ".join(f"{a} {b:.0f}" for a, b in zip(lab, dd)))
+    # L0 LayerNorms (C2 + stamps build): per wave, s_memtime at LN entry (its own GEMM done), after the partials
+    # barrier, after the statistics barrier and at exit, relative to the phase start (slots 32..63 LN1, 64..95 LN2)
+    for nm, base, p0, p1 in (("LN1", 32, 2, 3), ("LN2", 64, 3, 4)):
+        ln = sub[:, base:base + 32].reshape(-1, 8, 4)
+        if not ln.all():
+            continue
+        rel = (ln - sub[:, p0][:, None, None]).mean(axis=0)
+        end = (sub[:, p1] - sub[:, p0]).mean()
+        print(f"L0 {nm} per wave (cycles after the phase start; phase ends at {end:.0f}): "
+              "entry / after partials barrier / after stats barrier / exit")
+        for w in range(8):
+            print(f"    wave {w}: {rel[w, 0]:7.0f} {rel[w, 1]:7.0f} {rel[w, 2]:7.0f} {rel[w, 3]:7.0f}")
+        ent = ln[:, :, 0]
+        print(f"  {nm}: entry skew (last − first wave) mean {(ent.max(1) - ent.min(1)).mean():.0f}; "
+              f"last entry → partials barrier released {(ln[:, :, 1].min(1) - ent.max(1)).mean():.0f}; "
+              f"stats phase {(ln[:, :, 2].min(1) - ln[:, :, 1].max(1)).mean():.0f}; "
+              f"apply {(ln[:, :, 3] - ln[:, :, 2]).mean():.0f}; last exit → phase end "
+              f"{(sub[:, p1] - ln[:, :, 3].max(1)).mean():.0f}")
     e = sub[:, 124:128]
     if e[:, 0].any():
         pts = np.stack([e[:, 3], sub[:, 0], e[:, 0], e[:, 1], sub[:, 1]], axis=1)
