@@ -137,6 +137,7 @@ struct cet_engine {
   int last_path = 0; // the fused kernel the last forward launched (CET_PATH_*), 0: none yet
   std::string last_kernel;   // its instance, as rocprofv3 names it (cet_last_kernel)
   bool enc_split_ok = true;   // v4 encoder split allowed (CET_NO_ENC_SPLIT at creation turns it off)
+  bool feed_ok = false;       // the plan's decoder runs on the LDS-DMA weight feed (build_informer, FEED instances)
   int variant = 4;   // fused-kernel generation: 4 (one sequence per workgroup), the only one kept
   // shapes outside the fused kernels (d_model != 128, n_heads != 8, d_ff > 128, ...): the layer-wise
   // engine (cet_lw.hip), fp32 on the f32 MFMA, one launch per operator
@@ -714,6 +715,59 @@ int build_informer(cet_engine* e) {
     const auto& w = e->W("projection.weight");
     const auto& b = e->W("projection.bias");
     p.proj = pk.gemm(w, c.c_out, D, b.data(), nullptr);
+  }
+  // Decoder weight feed (cet_informer4.hpp FEED): the decoder's weight tiles stream into per-wave LDS slots by
+  // LDS-DMA, and its bias and LayerNorm vectors come from one 1 KiB parameter tile per (layer, wave) packed here
+  // after the weights, 16 blocks of the wave's 16 features: cross K / V, self K / V / Q, O biases, LN1 γ / β,
+  // cross Q, cross O biases, LN2 γ / β, FFN1 (n-tile w mod 4), FFN2 biases, LN3 γ / β.  Plans it fits: bf16
+  // operands, d_ff 64, a one-tile decoder (≤ 16 rows) whose ProbSparse calls select every query (u = L, the
+  // decoder of every BASELINE Informer config), and no per-output scales (LSQ plans keep the register path).
+  {
+    p.dec_par = NONE;
+    e->feed_ok = false;
+    bool scales = false;
+    for (int l = 0; l < c.d_layers; ++l) {
+      const DecLayerDesc& d = p.dec[l];
+      for (const GemmDesc* g : {&d.qkv, &d.o, &d.cq, &d.ckv, &d.co, &d.f1, &d.f2}) scales = scales || g->scale != NONE;
+    }
+    const bool dense_dec = !(c.attn_prob && u_part(c.factor, Ld) < Ld);
+    if (P == 0 && !scales && c.d_ff == 64 && Ld <= 16 && dense_dec && D == 128) {
+      while (wb.size() % 512) wb.push_back(0);   // 1 KiB aligned
+      p.dec_par = (uint32_t)(wb.size() / 8);
+      auto put = [&](float* t, int v, uint32_t off, int at) {
+        for (int i = 0; i < 16; ++i) t[16 * v + i] = off == NONE ? 0.f : pb[off + at + i];
+      };
+      for (int l = 0; l < c.d_layers; ++l) {
+        const DecLayerDesc& d = p.dec[l];
+        for (int w = 0; w < 8; ++w) {
+          float t[256];
+          put(t, 0, d.ckv.bias, 16 * w);
+          put(t, 1, d.ckv.bias, 128 + 16 * w);
+          put(t, 2, d.qkv.bias, 128 + 16 * w);
+          put(t, 3, d.qkv.bias, 256 + 16 * w);
+          put(t, 4, d.qkv.bias, 16 * w);
+          put(t, 5, d.o.bias, 16 * w);
+          put(t, 6, d.ln1.g, 16 * w);
+          put(t, 7, d.ln1.b, 16 * w);
+          put(t, 8, d.cq.bias, 16 * w);
+          put(t, 9, d.co.bias, 16 * w);
+          put(t, 10, d.ln2.g, 16 * w);
+          put(t, 11, d.ln2.b, 16 * w);
+          put(t, 12, d.f1.bias, 16 * (w % 4));
+          put(t, 13, d.f2.bias, 16 * w);
+          put(t, 14, d.ln3.g, 16 * w);
+          put(t, 15, d.ln3.b, 16 * w);
+          for (int i = 0; i < 256; ++i) {
+            uint32_t u;
+            std::memcpy(&u, &t[i], 4);
+            wb.push_back((uint16_t)(u & 0xffffu));
+            wb.push_back((uint16_t)(u >> 16));
+          }
+        }
+      }
+      e->feed_ok = std::getenv("CET_NO_FEED") == nullptr;   // CET_NO_FEED: the register path (A/B)
+    }
+    if (pk.wlo) pk.wlo->resize(wb.size(), 0);   // split bf16: the lo blob stays parallel (no tiles there)
   }
 
   // ProbSparse calls: multiplicity table layout + M debug dumps
@@ -1451,6 +1505,7 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   b.stagger = 0;
   if (const char* sg = std::getenv("CET_STAGGER")) b.stagger = std::atoi(sg);
   b.poison = lds_poison_requested();
+  b.feed = 0;
   b.enc_split = 0;
   b.enc_xchg = nullptr;
   b.enc_count = nullptr;
@@ -1488,10 +1543,12 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
     // the instance launch_v4 takes (v4_instance: one decision for both sides)
     const int inst = v4_instance(b, e->prec, e->icfg.d_ff);
     const int sh = inst == V4I_SHAPE || inst == V4I_SHAPE_STAMPS || (inst == V4I_SPLIT && b.shape == V4S_E43) ? b.shape : 0;
+    // the decoder weight feed: the bf16 shape instances (and E43's split form) of a plan build_informer accepted
+    b.feed = e->feed_ok && e->prec == 0 && sh != 0 ? 1 : 0;
     char nm[160];
-    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %d, %s>", e->icfg.d_ff,
+    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %d, %s, %s>", e->icfg.d_ff,
                   inst == V4I_DIAG ? "true" : "false", e->prec, inst == V4I_SPLIT ? "true" : "false", sh,
-                  inst == V4I_SHAPE_STAMPS ? "true" : "false");
+                  inst == V4I_SHAPE_STAMPS ? "true" : "false", b.feed ? "true" : "false");
     e->last_kernel = inst == V4I_NONE ? std::string() : std::string(nm);
   }
   return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);

@@ -21,7 +21,9 @@ namespace v4 {
 // 90 → 45 → 23 → 12 —, 2 the TimingAnalysis stack e_layers [4, 3] with a ≤ 16-row decoder over its 24 stack rows).
 // ST: a production instance that honours the phase stamps only (the C2 + stamps diagnostic build,
 // -DCET_C2_STAMPS: per-phase cycles of the instance the bench times).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false>
+// FEED: the decoder's weights and bias / LayerNorm vectors arrive by the LDS-DMA weight feed (cet_v4.hpp; the host
+// builds the parameter tiles and checks the plan: cet_api.cpp build_informer).
+template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false, bool FEED = false>
 __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(plan))
@@ -104,6 +106,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   f32x4 t0a = {0.f, 0.f, 0.f, 0.f}, t0b = t0a;
   int t0n = 0;   // 16-byte pieces of call 0's table (≤ 96 rows × 104 B / 16 = 624: two per thread)
   static_assert(LMAX * CNT_STRIDE / 16 <= 2 * NTHREADS, "call 0's table staged with two f32x4 per thread");
+  static_assert(!FEED || (P == P_BF16 && DFF == 64 && !DIAG && SH != V4S_GENERIC), "the feed's plans (cet_api.cpp)");
   if constexpr (PRE) {
     const int c0 = PL.enc[PL.enc_first[0]].call;
     if (a.cnt && c0 >= 0 && PL.calls[c0].u < PL.calls[c0].LQ) {
@@ -221,7 +224,10 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         // resident sampler: replay this call's draws into the LDS table (cet_mt.hpp)
         mt_replay<NTHREADS>(gen, c.LQ, c.U, c.LK, sparse ? reinterpret_cast<uint32_t*>(CNT) : nullptr,
                             c.cnt_stride);
-        if (call == PL.n_calls - 1 && b == 0) mt_store<NTHREADS>(gen, a.mt_out);
+        if (call == PL.n_calls - 1 && b == 0) {
+          mt_store<NTHREADS>(gen, a.mt_out);
+          if constexpr (FEED) vm_wait<0>();   // no store may stay in flight beside the feed's counted loads
+        }
       } else if (sparse && pre) {
         // staged earlier (C2): already in LDS behind an earlier barrier
       } else if (sparse) {
@@ -249,6 +255,86 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
     call_setup(io, call, pre);
     attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
+  };
+
+  // ---- decoder weight feed (FEED; cet_v4.hpp).  Per decoder layer and wave, 38 weight tiles in the order the
+  // layer consumes them — cross K (tiles 0-3), cross V (4-7), self K (8-11), self V (12-15), self Q (16-19),
+  // O (20-23), cross Q (24-27), cross O (28-31), FFN1 (32-35, n-tile w mod 4), FFN2 (36-37) — each in ring slot
+  // (2l + j) mod 6 of the wave, and the layer's parameter tile in the wave's parameter slot.  Past the last layer
+  // the stream continues with the projection's four tiles (then repeats: the counts stay static).
+  auto fd_rs = [&]() __attribute__((always_inline)) { return raw_rsrc(a.weights); };
+  auto fd_off = [&](int l, auto Jc) __attribute__((always_inline)) -> uint32_t {
+    constexpr int J = decltype(Jc)::value;
+    const uint32_t wv = (uint32_t)w;
+    if (l >= PL.d_layers) return PL.proj.w * 16u + (uint32_t)(J & 3) * 1024u;
+    if constexpr (J < 4) return PL.dec[l].ckv.w * 16u + (wv * 4u + J) * 1024u;
+    else if constexpr (J < 8) return PL.dec[l].ckv.w * 16u + ((8u + wv) * 4u + (J - 4)) * 1024u;
+    else if constexpr (J < 12) return PL.dec[l].qkv.w * 16u + ((8u + wv) * 4u + (J - 8)) * 1024u;
+    else if constexpr (J < 16) return PL.dec[l].qkv.w * 16u + ((16u + wv) * 4u + (J - 12)) * 1024u;
+    else if constexpr (J < 20) return PL.dec[l].qkv.w * 16u + (wv * 4u + (J - 16)) * 1024u;
+    else if constexpr (J < 24) return PL.dec[l].o.w * 16u + (wv * 4u + (J - 20)) * 1024u;
+    else if constexpr (J < 28) return PL.dec[l].cq.w * 16u + (wv * 4u + (J - 24)) * 1024u;
+    else if constexpr (J < 32) return PL.dec[l].co.w * 16u + (wv * 4u + (J - 28)) * 1024u;
+    else if constexpr (J < 36) return PL.dec[l].f1.w * 16u + ((wv & 3u) * 4u + (J - 32)) * 1024u;
+    else return PL.dec[l].f2.w * 16u + (wv * 2u + (J - 36)) * 1024u;
+  };
+  auto fd_slot = [&](int l, auto Jc) __attribute__((always_inline)) -> uint32_t {
+    constexpr int J = decltype(Jc)::value;
+    int k = (2 * l) % FEED_R + J % FEED_R;
+    k = k >= FEED_R ? k - FEED_R : k;
+    return feed_slot(FEED_R * w + k);
+  };
+  auto fd_issue = [&](int l, auto Tc) __attribute__((always_inline)) {   // tile T of layer l (T ≥ 38: of layer l + 1)
+    constexpr int T = decltype(Tc)::value;
+    if constexpr (T < 38) dma_tile(fd_rs(), fd_off(l, IC<T>{}), fd_slot(l, IC<T>{}), 16 * lane_op());
+    else dma_tile(fd_rs(), fd_off(l + 1, IC<T - 38>{}), fd_slot(l + 1, IC<T - 38>{}), 16 * lane_op());
+  };
+  auto fd_issue_par = [&](int l) __attribute__((always_inline)) {   // layer l's parameter tile (past the last: its copy)
+    const int lp = l < PL.d_layers ? l : PL.d_layers - 1;
+    dma_tile(fd_rs(), PL.dec_par * 16u + (uint32_t)(lp * NW + w) * 1024u, feed_slot(48 + w), 16 * lane_op());
+  };
+  // take K tiles J0 .. J0 + K − 1 of layer l (the caller waited for them), then refill their slots with the tiles
+  // six ahead in the stream
+  auto fd_read = [&](int l, auto J0c, auto Kc, auto* out) __attribute__((always_inline)) {
+    constexpr int J0 = decltype(J0c)::value, K = decltype(Kc)::value;
+    const int lane = lane_op();
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      uint32_t sl;
+      if (i == 0) sl = fd_slot(l, IC<J0>{});
+      else if (i == 1) sl = fd_slot(l, IC<J0 + 1>{});
+      else if (i == 2) sl = fd_slot(l, IC<J0 + 2>{});
+      else sl = fd_slot(l, IC<J0 + 3>{});
+      out[i].h = *reinterpret_cast<const bf16x8*>(lds + sl + 16 * lane);   // (bf16 fragments: FEED is P_BF16)
+    }
+  };
+  auto fd_take = [&](int l, auto J0c, auto Kc, auto* out) __attribute__((always_inline)) {
+    constexpr int J0 = decltype(J0c)::value, K = decltype(Kc)::value;
+    fd_read(l, J0c, Kc, out);
+    lgkm_wait0();   // the slots are read before they are refilled
+    fd_issue(l, IC<J0 + FEED_R>{});
+    fd_issue(l, IC<J0 + FEED_R + 1>{});
+    if constexpr (K > 2) {
+      fd_issue(l, IC<J0 + FEED_R + 2>{});
+      fd_issue(l, IC<J0 + FEED_R + 3>{});
+    }
+  };
+  auto fd_par4 = [&](int v) __attribute__((always_inline)) {   // block v, the lane group's four features
+    return *reinterpret_cast<const f32x4*>(lds + feed_slot(48 + w) + (16 * v + 4 * (lane_op() >> 4)) * 4);
+  };
+  auto fd_par1 = [&](int v) __attribute__((always_inline)) {   // block v, feature (lane & 15)
+    return *reinterpret_cast<const float*>(lds + feed_slot(48 + w) + (16 * v + (lane_op() & 15)) * 4);
+  };
+  // the stream's first six tiles and layer 0's parameter tile, issued well ahead of the decoder (the encoder
+  // norm phase; under the encoder split after the stack-output exchange)
+  auto fd_prefill = [&]() __attribute__((always_inline)) {
+    fd_issue(0, IC<0>{});
+    fd_issue(0, IC<1>{});
+    fd_issue(0, IC<2>{});
+    fd_issue(0, IC<3>{});
+    fd_issue(0, IC<4>{});
+    fd_issue(0, IC<5>{});
+    fd_issue_par(0);
   };
 
   for (int e = 0; e < PL.n_enc; ++e) {
@@ -419,6 +505,9 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     nmt = (L + 15) >> 4;
     // ---- Encoder.norm (encoder.py:83-84) → this encoder's rows of the stack output (ENC)
     const int rows = PL.enc_rows[e];
+    if constexpr (FEED && !SPLIT) {
+      if (e == PL.n_enc - 1) fd_prefill();
+    }
     const ImgRows<P> encw{ENC, PL.enc_row_off[e]};
     ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, XB, &encw);
     __syncthreads();
@@ -461,11 +550,185 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
         encw[r0 * RW + i] = __hip_atomic_load(xchg + r0 * RW + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    if constexpr (FEED) fd_prefill();   // the exchange's stores are retired (vmcnt(0) above)
   }
   if (xdec_off < 0) {   // no room to keep it since entry: stage it now (into CTX, free after the encoder)
     stage(a.x_dec + (size_t)b * Ld * C, XDEC, Ld, C, CS);
     __syncthreads();
   }
+  // ---- the decoder on the weight feed (FEED): the decoder below, with every weight tile taken from the wave's LDS
+  //      ring (six tiles ahead) and every bias / LayerNorm vector from the layer's parameter tile — no global load
+  //      of the decoder layers waits in a phase.  The counted waits follow the stream: entering a layer 7 loads
+  //      are in flight (tiles 0-5, the parameter tile); each group of four leaves two in flight, FFN2's pair four.
+  auto decoder_feed = [&](auto NMSc) __attribute__((always_inline)) {
+   if constexpr (FEED) {
+    constexpr int NMS = decltype(NMSc)::value;
+    constexpr bool CROSS_EXACT = NMS == 1 || SH == V4S_E43;
+    constexpr int NMD = 1;
+    const int nmd = NMD;
+    Res<NMD> XD;
+    {
+      const GemmDesc d = PL.emb_dec;
+      gemm_res_n<PP, 2, NMD>(M, d, LoadEmbed<PP>{XDEC, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
+        const int m = mt * 16 + (lane_op() & 15);
+        const int prow = m < LMAX ? m : LMAX - 1;
+        XD.v[mt] = y + pload4(M, PL.pe_dec, prow * DMODEL + n0);
+      });
+    }
+    __syncthreads();
+    store_res(XD, nmd, Ld, XB);
+    __syncthreads();
+    STAMP();  // decoder embedding
+    const f32x4 one4 = {1.f, 1.f, 1.f, 1.f};
+    for (int l = 0; l < PL.d_layers; ++l) {
+      // cross-attention K / V of this layer (the encoder-stack output only), projected first
+      KVPre<P> ckv;
+      vm_wait<3>();
+      fd_take(l, IC<0>{}, IC<4>{}, ckv.k);
+      vm_wait<2>();
+      fd_take(l, IC<4>{}, IC<4>{}, ckv.v);
+      ckv.sk = one4;
+      ckv.bk = fd_par4(0);
+      ckv.sv = 1.f;
+      ckv.bv = fd_par1(1);
+      const HeadIO<P> cio = head_io(XB, ENC, 0u, 0u, 0u, GemmDesc{}, GemmDesc{}, GemmDesc{}, Ld, S, 0, 0, 0, nullptr);
+      AF<PP> CK[NMS], CV[NMS];
+      project_kv<P, NMS>(cio, ckv, CK, CV);
+      {
+        // masked self-attention with the mix scramble (model.py:211-222); every query selected (u = L)
+        HeadIO<P> sio = head_io(XB, XB, 0u, 0u, 0u, GemmDesc{}, GemmDesc{}, GemmDesc{}, Ld, Ld, PL.prob, 1, PL.mix,
+                                nullptr);
+        call_setup(sio, DLD.call, nullptr);   // the draws still advance the sampler stream
+        KVPre<P> skv;
+        vm_wait<2>();
+        fd_take(l, IC<8>{}, IC<4>{}, skv.k);
+        vm_wait<2>();
+        fd_take(l, IC<12>{}, IC<4>{}, skv.v);
+        skv.sk = one4;
+        skv.bk = fd_par4(2);
+        skv.sv = 1.f;
+        skv.bv = fd_par1(3);
+        AF<PP> SK[NMD], SV[NMD];
+        project_kv<P, NMD>(sio, skv, SK, SV);
+        WPre<P, 4> sq;
+        vm_wait<2>();
+        fd_take(l, IC<16>{}, IC<4>{}, sq.a);
+        sq.sc = one4;
+        sq.bi = fd_par4(4);
+        attention_head<P, NMD, NMD, true, true>(sio, M, w, SK, SV, &sq);
+      }
+      WPre<P, 4> po;
+      vm_wait<2>();
+      fd_take(l, IC<20>{}, IC<4>{}, po.a);
+      po.sc = one4;
+      po.bi = fd_par4(5);
+      __syncthreads();
+      STAMP();  // decoder self-attention
+      gemm_res_n<P, 4, NMD>(po, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      WPre<P, 4> pcq;
+      vm_wait<2>();
+      fd_take(l, IC<24>{}, IC<4>{}, pcq.a);
+      pcq.sc = one4;
+      pcq.bi = fd_par4(8);
+      ln_res_gb(XD, nmd, Ld, fd_par4(6), fd_par4(7), 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      // cross-attention: FullAttention over the encoder-stack output, mix=False
+      attention_head<P, NMD, NMS, true, CROSS_EXACT>(cio, M, w, CK, CV, &pcq);
+      WPre<P, 4> pco;
+      vm_wait<2>();
+      fd_take(l, IC<28>{}, IC<4>{}, pco.a);
+      pco.sc = one4;
+      pco.bi = fd_par4(9);
+      __syncthreads();
+      STAMP();  // cross-attention
+      gemm_res_n<P, 4, NMD>(pco, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      WPre<P, 4> pf1;
+      vm_wait<2>();
+      fd_take(l, IC<32>{}, IC<4>{}, pf1.a);   // refills the next layer's tiles 0-3 (or the projection's)
+      pf1.sc = one4;
+      pf1.bi = fd_par4(12);
+      ln_res_gb(XD, nmd, Ld, fd_par4(10), fd_par4(11), 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      __syncthreads();
+      {
+        const int relu = PL.act_relu;
+        gemm_tiles1<P, 4>(pf1, DFF / 16, nmd, LoadImg<P>{XB}, [&](int mt, int n0, f32x4 v) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
+          CTXI.st4(mt * 16 + (lane_op() & 15), n0, v);
+        });
+      }
+      WPre<P, DFF / 32> pf2;
+      vm_wait<4>();
+      fd_take(l, IC<36>{}, IC<2>{}, pf2.a);   // refills the next layer's tiles 4-5
+      pf2.sc = one4;
+      pf2.bi = fd_par4(13);
+      __syncthreads();
+      gemm_res_n<P, DFF / 32, NMD>(pf2, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      ln_res_gb(XD, nmd, Ld, fd_par4(14), fd_par4(15), 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      lgkm_wait0();          // the parameter tile's last reads are done ...
+      fd_issue_par(l + 1);   // ... before the next layer's tile replaces it
+      __syncthreads();
+      STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3
+    }
+    // final norm → the projection's input image (plain precision; CTX rows < 16 are free: FFN2 is done)
+    ln_res(XD, nmd, Ld, M, PL.dec_norm, 1e-5f, false, LNP, FIN, (const Img<PP>*)nullptr);
+    __syncthreads();
+    {
+      // projection (model.py:264) on the last pred_len rows → out[b]: the stream's four tiles past the last layer
+      WF<P> pw[4];
+      vm_wait<0>();   // the stream is drained (its last three loads are dummies): nothing stays in flight past here
+      fd_read(PL.d_layers, IC<0>{}, IC<4>{}, pw);
+      const GemmDesc d = PL.proj;
+      const int first_row = Ld - PL.pred_len, co = PL.c_out;
+      float* out = a.out + (size_t)b * PL.pred_len * co;
+#ifdef V4_NO_FUSE
+      constexpr bool fuse = false;
+#else
+      const bool fuse = a.label != nullptr;
+#endif
+      if (w == 0) {   // one n-tile (c_out ≤ 16), one m-tile: wave 0
+        const int lane = lane_op();
+        const int kq = kq_of<PP>(lane), mrow = lane & 15;
+        const int n0 = (lane >> 4) * 4;
+        f32x4 sc, bi;
+        epi_vecs(M, d, n0, sc, bi);
+        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) c = mma<PP>(&pw[ks], FIN.ld(mrow, ks * 32 + kq), c);
+        const f32x4 v = c * sc + bi;
+        const int m = mrow;
+        const bool valid = m >= first_row && m < Ld;
+        float se = 0.f, pwr = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (valid && n0 + r < co) {
+            out[(m - first_row) * co + n0 + r] = v[r];
+            if (fuse) {   // NMSE_Split_cuda(x_hat = out, x = label): Σ(x − x̂)², Σ x̂² (metrics.py:26-30)
+              const float dx = LAB[(m - first_row) * co + n0 + r] - v[r];
+              se = fmaf(dx, dx, se);
+              pwr = fmaf(v[r], v[r], pwr);
+            }
+          }
+        if (fuse) {
+          se = xor_sum(se, 16);
+          se = xor_sum(se, 32);
+          pwr = xor_sum(pwr, 16);
+          pwr = xor_sum(pwr, 32);
+          if ((lane >> 4) == 0 && valid) {
+            const float2 pr = make_float2(se, pwr);
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.nmse_part + (size_t)b * PL.pred_len +
+                                                                     (m - first_row)),
+                               __builtin_bit_cast(unsigned long long, pr), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        if (fuse) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are done
+      }
+    }
+    STAMP();  // final norm + projection
+    if (stamps && threadIdx.x == 0) stamps[99] = __builtin_amdgcn_s_memrealtime();
+   }
+  };
   auto decoder = [&](auto NMDc, auto NMSc) __attribute__((always_inline)) {
     constexpr int NMS = decltype(NMSc)::value;
     // the cross-attention's key-tile bound is exact for one tile (S ≤ 16) and in the E43 instance (S = 24)
@@ -605,7 +868,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     STAMP();  // final norm + projection
     if (stamps && threadIdx.x == 0) stamps[99] = __builtin_amdgcn_s_memrealtime();
   };
-  if constexpr (SH == V4S_E43) {
+  if constexpr (FEED) {
+    // the host checks the plan (cet_api.cpp build_informer): a one-tile decoder; C2's stack output is one tile (S =
+    // 12), the E43 stack's two (S = 24)
+    decoder_feed(IC<SH == V4S_E43 ? 2 : 1>{});
+  } else if constexpr (SH == V4S_E43) {
     decoder(IC<1>{}, IC<2>{});   // the host checks dec_len ≤ 16 and S = 24
   } else switch ((Ld + 15) >> 4) {
     case 1: S <= 16 ? decoder(IC<1>{}, IC<1>{}) : decoder(IC<1>{}, IC<MT>{}); break;
@@ -697,10 +964,10 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 }
 
 // X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false, bool FEED = false>
 __global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
     informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
-  informer_forward_v4_body<DFF, DIAG, P, SPLIT, SH, ST>(a, plan);
+  informer_forward_v4_body<DFF, DIAG, P, SPLIT, SH, ST, FEED>(a, plan);
 }
 
 template <int P>
@@ -712,22 +979,32 @@ int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream)
   switch (v4_instance(*a, P, dff)) {
     case V4I_SPLIT:   // encoder split: bf16 policy, production instance only (the launcher checks the plan)
       if constexpr (P == P_BF16) {
-        if (a->shape == V4S_E43) kern = informer_forward_v4<64, false, P, true, V4S_E43>;
+        if (a->shape == V4S_E43)
+          kern = a->feed ? informer_forward_v4<64, false, P, true, V4S_E43, false, true>
+                         : informer_forward_v4<64, false, P, true, V4S_E43>;
         else kern = dff == 64 ? informer_forward_v4<64, false, P, true> : informer_forward_v4<128, false, P, true>;
       }
       break;
 #ifdef CET_C2_STAMPS
     case V4I_SHAPE_STAMPS:   // the shape instance + phase stamps (diagnostic build)
       if constexpr (P == P_BF16) {
-        kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43, true>
-                                   : informer_forward_v4<64, false, P, false, V4S_C2, true>;
+        if (a->feed)
+          kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43, true, true>
+                                     : informer_forward_v4<64, false, P, false, V4S_C2, true, true>;
+        else
+          kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43, true>
+                                     : informer_forward_v4<64, false, P, false, V4S_C2, true>;
       }
       break;
 #endif
     case V4I_SHAPE:   // the plan's rows at compile time
       if constexpr (P == P_BF16) {
-        kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43>
-                                   : informer_forward_v4<64, false, P, false, V4S_C2>;
+        if (a->feed)   // the decoder on the LDS-DMA weight feed (the host checked the plan)
+          kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43, false, true>
+                                     : informer_forward_v4<64, false, P, false, V4S_C2, false, true>;
+        else
+          kern = a->shape == V4S_E43 ? informer_forward_v4<64, false, P, false, V4S_E43>
+                                     : informer_forward_v4<64, false, P, false, V4S_C2>;
       } else if constexpr (P == P_FP8) {
         kern = informer_forward_v4<64, false, P, false, V4S_C2>;
       }

@@ -43,6 +43,7 @@ struct InformerArgs {
   int shape;                  // v4_shape of the plan (V4S_*): the bf16 production launch takes the instance with its
                               // encoder rows as compile-time constants
   int poison;                 // diagnostic (CET_LDS_POISON=1): every LDS byte NaN at entry, before anything is staged
+  int feed;                   // the plan's decoder runs on the LDS-DMA weight feed (the FEED instances)
 };
 
 // Plans with a compile-time instance (cet_api.cpp plan_shape): C2's encoder (one encoder, rows 90 → 45 → 23 → 12,

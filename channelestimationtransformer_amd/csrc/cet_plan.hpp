@@ -96,6 +96,7 @@ struct InformerPlan {
   int in_stride;            // floats per staged input row
   int dbg_stride, dbg_emb, dbg_dec_emb, dbg_dec_out;
   int draws;                // mt19937 words one forward consumes (Σ LQ·U over every call)
+  uint32_t dec_par;         // decoder weight feed: 16-byte-unit offset of the (layer, wave) parameter tiles, or NONE
 };
 
 // v4 LDS layout (precision P: 0 bf16, 1 split-bf16 hi/lo planes, 2 fp8); every offset the kernel

@@ -381,6 +381,54 @@ struct Res {
   f32x4 v[N];
 };
 
+// ------------------------------------------------------------------ decoder weight feed (LDS-DMA)
+// The decoder's weight tiles (1 KiB wave tiles of the fragment blob) stream into per-wave LDS slots with
+// buffer_load_dwordx4 … lds (no VGPR destination), six tiles ahead of their use, and its bias / LayerNorm
+// vectors arrive the same way as one 1 KiB parameter tile per (layer, wave) (cet_api.cpp build_informer).  The
+// slots live in LDS the decoder leaves unused (bf16 layout): image rows 16–95 of XB and of CTX, the LayerNorm
+// partials past row 15 and the multiplicity table — 57 slots; wave w owns ring slots 6w .. 6w + 5 and
+// parameter slot 48 + w.  hipcc does not count these loads: the issuing wave retires them with its own counted
+// s_waitcnt vmcnt and reads only its own slots, so no barrier orders them.
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4u32 raw_rsrc(const void* base) {   // the descriptor make_rsrc builds, as a value
+  const uint64_t p = (uint64_t)base;
+  return v4u32{(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)p),
+               (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)(p >> 32) & 0xffffu)), 0x7ffffff0u, 0x00020000u};
+}
+// one 1 KiB wave tile at blob byte offset soff → LDS bytes [dst, dst + 1024): lane l's 16 bytes at dst + 16·l
+__device__ __forceinline__ void dma_tile(v4u32 rsrc, uint32_t soff, uint32_t dst, int voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(dst), "s"(soff)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+constexpr int FEED_R = 6;   // ring tiles per wave
+constexpr uint32_t FEED_XB = 16 * V4_RS16;                                  // XB rows 16..95: 21 slots
+constexpr uint32_t FEED_CTX = (uint32_t)v4_ctx(0) + 16 * V4_RS16;           // CTX rows 16..95: 21 slots
+constexpr uint32_t FEED_SCR = (uint32_t)v4_scr(0) + 16 * LN_STRIDE * 4;    // LN partials past row 15: 6 slots
+constexpr uint32_t FEED_CNT = (uint32_t)v4_cnt(0);                          // the multiplicity table: 9 slots
+static_assert(FEED_XB + 21 * 1024 <= (uint32_t)v4_ctx(0), "XB slots inside XB");
+static_assert(FEED_CTX + 21 * 1024 <= (uint32_t)v4_scr(0), "CTX slots inside CTX");
+static_assert(FEED_SCR + 6 * 1024 <= (uint32_t)v4_scr(0) + LMAX * LN_STRIDE * 4, "slots below the LN statistics");
+static_assert(FEED_CNT + 8 * 1024 <= (uint32_t)v4_enc(0), "CNT slots inside the table");
+__device__ __forceinline__ uint32_t feed_slot(int i) {
+  return i < 21 ? FEED_XB + 1024u * i
+       : i < 42 ? FEED_CTX + 1024u * (i - 21)
+       : i < 48 ? FEED_SCR + 1024u * (i - 42)
+                : FEED_CNT + 1024u * (i - 48);
+}
+
 // A dense layer's per-wave operands, requested ahead of the barrier that precedes the layer.
 template <int P, int KS>
 struct WPre {
@@ -626,10 +674,12 @@ __device__ __forceinline__ void ln_apply_own(Res<N>& X, int nmt, int rows, f32x4
 // normalised rows only go to the image(s); X keeps the residual.
 // lst (diagnostics, the C2 + stamps build): per-wave s_memtime at entry, after each barrier and at exit, in
 // lst[4·w + 0..3] — which part of a LayerNorm phase is the wave's own work and which is waiting for the others.
+// ln_res_gb: γ / β of the wave's four features given (the decoder weight feed reads them from its parameter
+// tile); ln_res below loads them from the parameter blob.
 template <int N, class Out, class Out2, bool INPLACE = true>
-__device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
-                                       bool unbiased_std, float* part, const Out& out, const Out2* out2,
-                                       unsigned long long* lst = nullptr) {
+__device__ __forceinline__ void ln_res_gb(Res<N>& X, int nmt, int rows, const f32x4 g0, const f32x4 b0, float eps,
+                                          bool unbiased_std, float* part, const Out& out, const Out2* out2,
+                                          unsigned long long* lst = nullptr) {
   const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
   const int nb = 16 * w + 4 * g;
   float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
@@ -637,7 +687,6 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     if (lst && lane == 0) lst[4 * w + k] = __builtin_amdgcn_s_memtime();
   };
   LST(0);
-  const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
 #ifdef CET_ABL_LN
   // ablation (wrong results): no row statistics, no barriers — the LayerNorm's own cost, measured by its absence
   (void)part; (void)stats; (void)eps; (void)unbiased_std;
@@ -727,6 +776,14 @@ __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& 
     }
   }
   LST(3);
+}
+template <int N, class Out, class Out2, bool INPLACE = true>
+__device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
+                                       bool unbiased_std, float* part, const Out& out, const Out2* out2,
+                                       unsigned long long* lst = nullptr) {
+  const int nb = 16 * wave_id() + 4 * (lane_op() >> 4);
+  const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
+  ln_res_gb<N, Out, Out2, INPLACE>(X, nmt, rows, g0, b0, eps, unbiased_std, part, out, out2, lst);
 }
 
 // Two torch.nn.LayerNorms under one barrier, both in the own-rows form: the fused decoder layer 0's LN1

@@ -473,8 +473,8 @@ def test_encoder_split_e43_rows_with_dff128_vs_oracle():
     m.eval()
     state = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
     orc = InformerOracle(InformerConfig(e_layers=(4, 3), d_ff=128, attn="full"), state)
-    for B, kernel in ((64, "cet::v4::informer_forward_v4<128, false, 0, true, 0, false>"),
-                      (300, "cet::v4::informer_forward_v4<128, false, 0, false, 0, false>")):
+    for B, kernel in ((64, "cet::v4::informer_forward_v4<128, false, 0, true, 0, false, false>"),
+                      (300, "cet::v4::informer_forward_v4<128, false, 0, false, 0, false, false>")):
         xe, xd, _ = make_batch(B, seed=500 + B)
         with torch.no_grad():
             res = m(torch.from_numpy(xe).to(dev), range(90), torch.from_numpy(xd).to(dev), range(15))
@@ -743,9 +743,10 @@ def test_fused_nmse_odd_batch_and_label_width(c_out):
     np.testing.assert_allclose((s[0] / s[1]).cpu().numpy(), ref_split(o.cpu().numpy(), lab_np), rtol=1e-5)
 
 
-C2_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, 1, false>"     # plan_shape V4S_C2
-E43_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, 2, false>"    # V4S_E43 (TimingAnalysis stack)
-E43_SPLIT_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, true, 2, false>"
+# the shape instances with the decoder on the LDS-DMA weight feed (the last template argument)
+C2_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, true>"     # plan_shape V4S_C2
+E43_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, false, 2, false, true>"    # V4S_E43 (TimingAnalysis stack)
+E43_SPLIT_KERNEL = "cet::v4::informer_forward_v4<64, false, 0, true, 2, false, true>"
 
 
 def _c2_model(attn, seed, bias_offset=0.0):
@@ -810,3 +811,50 @@ def test_layernorm_rows_with_a_large_mean_offset(offset):
     assert m.engine(torch.device("cuda:0")).last_kernel() == C2_KERNEL
     ref, _ = InformerOracle(InformerConfig(attn="full"), state).forward(xe, xd, ())
     assert rel_nmse(out, ref) < TOL, rel_nmse(out, ref)
+
+
+@pytest.mark.parametrize("which,B", [("c2-prob", 512), ("c2-full", 512), ("e43", 512), ("e43", 40)])
+def test_decoder_feed_bitwise_equals_register_path(which, B):
+    """The decoder on the LDS-DMA weight feed (weight tiles six ahead in per-wave LDS slots, bias / LayerNorm
+    vectors from a per-(layer, wave) parameter tile) computes exactly what the register path computes: the same
+    bytes in the same MFMAs and epilogues.  Each plan runs with the feed and with CET_NO_FEED (the register
+    path, a separately built engine) on the same inputs and draws: outputs bitwise equal, the instance asserted
+    by name.  C2 under both attention modes at B = 512, the TimingAnalysis stack at B = 512 and in its
+    encoder-split form (B = 40)."""
+    _gpu()
+    import os
+
+    from channelestimationtransformer_amd.dataset import make_batch
+    from channelestimationtransformer_amd.informer import InformerStack
+    from channelestimationtransformer_amd.rng import draw_indices
+    from channelestimationtransformer_amd.weights import synthetic_state_dict
+    from engine_util import run_engine
+    from oracle.informer_np import InformerConfig, sample_shapes
+
+    dev = torch.device("cuda:0")
+    attn = "prob" if which == "c2-prob" else "full"
+    e_layers = [4, 3] if which == "e43" else [4]
+
+    def build():
+        m = InformerStack(16, 16, 16, 90, 10, 5, 5, 128, 8, e_layers, 3, 64, 0.05, attn, "fixed", "gelu", False,
+                          True, dev)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(m._schema(), 12).items()})
+        return m.eval()
+
+    idx = draw_indices(sample_shapes(InformerConfig(attn=attn, e_layers=tuple(e_layers))), seed=5) \
+        if attn == "prob" else None
+    xe, xd, _ = make_batch(B, seed=610 + B)
+    m = build()
+    out, _, _ = run_engine(m, xe, xd, idx)
+    name = m.engine(dev).last_kernel()
+    assert name.endswith(", true>"), name
+    os.environ["CET_NO_FEED"] = "1"
+    try:
+        m2 = build()
+        ref, _, _ = run_engine(m2, xe, xd, idx)
+        name2 = m2.engine(dev).last_kernel()
+    finally:
+        del os.environ["CET_NO_FEED"]
+    assert name2 == name[:-len(", true>")] + ", false>", (name, name2)
+    assert np.isfinite(out).all()
+    np.testing.assert_array_equal(out, ref)
