@@ -765,7 +765,9 @@ int build_informer(cet_engine* e) {
           }
         }
       }
-      e->feed_ok = std::getenv("CET_NO_FEED") == nullptr;   // CET_NO_FEED: the register path (A/B)
+      // opt-in (CET_FEED=1): measured slower than the register path — LDS-DMA fills ≈12 B/clk per CU against the
+      // decoder's ≈40 B/clk of weights, and the weights' L2 latency is mostly hidden already
+      e->feed_ok = std::getenv("CET_FEED") != nullptr;
     }
     if (pk.wlo) pk.wlo->resize(wb.size(), 0);   // split bf16: the lo blob stays parallel (no tiles there)
   }
@@ -826,6 +828,8 @@ int build_informer(cet_engine* e) {
     }
     p.lds4_lab = p.lds4_bytes;
     p.lds4_bytes = al(p.lds4_bytes + c.out_len * c.c_out * 4);
+    p.lds4_lncnt = p.lds4_bytes;
+    p.lds4_bytes = al(p.lds4_bytes + 16);
     p.lds4_mt = p.lds4_bytes;
     p.lds4_bytes_replay = al(p.lds4_mt + MT_WORDS_HOST * 4);
     if (LMAX * p.in_stride * 4 > v4_ctx_bytes(P) || Ld > 48 || p.lds4_bytes_replay > 160 * 1024)

@@ -57,6 +57,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   const Img<P> ENC{lds + v4_enc(P), PL.lds4_enc_lo};                    // encoder-stack output
   const Img<PP> FIN{lds + v4_ctx(P), Geo<PP>::IMG};                      // decoder output (projection input)
   float* LNP = reinterpret_cast<float*>(lds + v4_scr(P));            // LN partials (alias the scratch)
+#ifdef CET_LN_LAST
+  unsigned* LNC = reinterpret_cast<unsigned*>(lds + PL.lds4_lncnt);  // LayerNorm arrival counter
+  if (threadIdx.x == 0) *LNC = 0u;   // ordered before the first LayerNorm by the encoder loop's barriers
+#else
+  unsigned* LNC = nullptr;
+#endif
   uint8_t* CNT = reinterpret_cast<uint8_t*>(lds + v4_cnt(P));
   MTState gen{reinterpret_cast<uint32_t*>(lds + PL.lds4_mt), MT_N};
   float* SCR = reinterpret_cast<float*>(lds + v4_scr(P)) + w * SCR_FLOATS;
@@ -253,8 +259,16 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     constexpr bool NKX_ = decltype(NKXc)::value;
     HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
+#ifdef CET_AB8
+    // reproduction of round 4's ab8 candidate: the head's K/V weights requested before
+    // the call's table setup; it made the split-bf16 production instance disagree with its diagnostic one
+    const KVPre<P> kvp = prefetch_kv<P>(io, M, w);
+    call_setup(io, call, pre);
+    attention_head<P, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
+#else
     call_setup(io, call, pre);
     attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
+#endif
   };
 
   // ---- decoder weight feed (FEED; cet_v4.hpp).  Per decoder layer and wave, 38 weight tiles in the order the
@@ -423,7 +437,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       static_assert(DFF / 16 <= NW, "FFN hidden n-tiles: at most one per wave");
       const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, ELD.f1, DFF / 16);   // conv1 (k=1) + activation
       ln_res(X, nmt, L, M, ELD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr,
-             ST && stamps && e == 0 && l == 0 ? stamps + 32 : nullptr);   // L0 LN1 per-wave stamps: slots 32..63
+             ST && stamps && e == 0 && l == 0 ? stamps + 32 : nullptr, LNC);   // L0 LN1 per-wave stamps: 32..63
       __syncthreads();
       STAMP();  // out-projection + LN1
       {
@@ -443,7 +457,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       const int has_conv = ELD.conv.n;
       const bool last_of_stack = e == PL.n_enc - 1 && l == PL.enc_layers[e] - 1;
       ln_res(X, nmt, L, M, ELD.ln2, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr,
-             ST && stamps && e == 0 && l == 0 ? stamps + 64 : nullptr);   // L0 LN2: slots 64..95
+             ST && stamps && e == 0 && l == 0 ? stamps + 64 : nullptr, LNC);   // L0 LN2: slots 64..95
       __syncthreads();
       STAMP();  // FFN + LN2
       if (dbg && ELD.dbg_layer >= 0) dump_res(X, nmt, L, dbg + ELD.dbg_layer);
@@ -509,7 +523,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       if (e == PL.n_enc - 1) fd_prefill();
     }
     const ImgRows<P> encw{ENC, PL.enc_row_off[e]};
-    ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, XB, &encw);
+    ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, XB, &encw, nullptr, LNC);
     __syncthreads();
     if (dbg && PL.enc_dbg[e] >= 0) dump_res(X, nmt, rows, dbg + PL.enc_dbg[e]);
     STAMP();  // encoder norm

@@ -91,6 +91,7 @@ struct InformerPlan {
   int lds4_enc, lds4_enc_lo, lds4_cnt, lds4_mt, lds4_zero, lds4_bytes, lds4_bytes_replay;
   int lds4_xdec;            // x_dec staged at kernel entry (byte offset), or -1: staged before the decoder
   int lds4_lab;             // labels of the fused NMSE (pred_len × c_out fp32), staged at kernel entry
+  int lds4_lncnt;           // LayerNorm arrival counter (-DCET_LN_LAST: the last wave to publish combines the rows)
   int prec;                 // v4 operand precision of the dense layers (v4::P_BF16 / P_X3 / P_FP8)
   int stack;
   int in_stride;            // floats per staged input row

@@ -679,7 +679,7 @@ __device__ __forceinline__ void ln_apply_own(Res<N>& X, int nmt, int rows, f32x4
 template <int N, class Out, class Out2, bool INPLACE = true>
 __device__ __forceinline__ void ln_res_gb(Res<N>& X, int nmt, int rows, const f32x4 g0, const f32x4 b0, float eps,
                                           bool unbiased_std, float* part, const Out& out, const Out2* out2,
-                                          unsigned long long* lst = nullptr) {
+                                          unsigned long long* lst = nullptr, unsigned* arrive = nullptr) {
   const int lane = lane_op(), w = wave_id(), g = lane >> 4, c = lane & 15;
   const int nb = 16 * w + 4 * g;
   float* stats = part + LMAX * LN_STRIDE;   // [LMAX] (mean, 1/std): the scratch's last 768 bytes
@@ -703,6 +703,42 @@ __device__ __forceinline__ void ln_res_gb(Res<N>& X, int nmt, int rows, const f3
     }
   }
   return;
+#endif
+#ifdef CET_LN_LAST
+  if constexpr (N > 1) {
+    if (arrive) {
+      // one barrier instead of two: each wave counts itself in after publishing its partials (LDS executes a
+      // wave's operations in order, so the count follows its stores), and the last to arrive combines every row
+      // and re-arms the counter before the barrier
+      ln_publish(X, nmt, part);
+      unsigned t = 0;
+      if (lane == 0) t = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+      if (t == (unsigned)(NW - 1)) {
+        for (int m = lane; m < nmt * 16; m += WAVE)
+          *reinterpret_cast<f32x2*>(stats + 2 * m) = ln_row_stats(part, m, eps, unbiased_std);
+        if (lane == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __syncthreads();
+      LST(1);
+      LST(2);
+#pragma unroll
+      for (int mt = 0; mt < N; ++mt) {
+        if (mt < nmt) {
+          const int m = mt * 16 + c;
+          const f32x2 st = *reinterpret_cast<const f32x2*>(stats + 2 * m);
+          const f32x4 y = (X.v[mt] - st[0]) * st[1] * g0 + b0;
+          if (INPLACE) X.v[mt] = y;
+          if (m < rows) {
+            out.st4(m, nb, y);
+            if (out2) out2->st4(m, nb, y);
+          }
+        }
+      }
+      LST(3);
+      return;
+    }
+  }
 #endif
 #ifndef CET_LN_TWOPASS
   ln_publish(X, nmt, part);
@@ -780,10 +816,10 @@ __device__ __forceinline__ void ln_res_gb(Res<N>& X, int nmt, int rows, const f3
 template <int N, class Out, class Out2, bool INPLACE = true>
 __device__ __forceinline__ void ln_res(Res<N>& X, int nmt, int rows, const Mem& mm, const LNDesc ln, float eps,
                                        bool unbiased_std, float* part, const Out& out, const Out2* out2,
-                                       unsigned long long* lst = nullptr) {
+                                       unsigned long long* lst = nullptr, unsigned* arrive = nullptr) {
   const int nb = 16 * wave_id() + 4 * (lane_op() >> 4);
   const f32x4 g0 = pload4(mm, ln.g, nb), b0 = pload4(mm, ln.b, nb);   // issued before the barriers
-  ln_res_gb<N, Out, Out2, INPLACE>(X, nmt, rows, g0, b0, eps, unbiased_std, part, out, out2, lst);
+  ln_res_gb<N, Out, Out2, INPLACE>(X, nmt, rows, g0, b0, eps, unbiased_std, part, out, out2, lst, arrive);
 }
 
 // Two torch.nn.LayerNorms under one barrier, both in the own-rows form: the fused decoder layer 0's LN1
@@ -1033,7 +1069,8 @@ template <int PD, int MQ = MT, int MK = MT, bool EXTKV = false, bool NKX = false
 __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& m, int h,
                                                const AF<plain_of<PD>()>* kin = nullptr,
                                                const AF<plain_of<PD>()>* vin = nullptr,
-                                               const WPre<PD, 4>* qpre = nullptr) {
+                                               const WPre<PD, 4>* qpre = nullptr,
+                                               const KVPre<PD>* kvpre = nullptr) {
   constexpr int PA = plain_of<PD>();
   const int lane = lane_op();
   const int col = lane & 15, g = lane >> 4;
@@ -1070,6 +1107,8 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       Kf[mt] = kin[mt];
       Vf[mt] = vin[mt];
     }
+  } else if (kvpre) {
+    project_kv<PD, MK>(io, *kvpre, Kf, Vf);   // weights requested by the caller (the CET_AB8 reproduction)
   } else {
     project_kv<PD, MK>(io, m, h, Kf, Vf);
   }

@@ -206,7 +206,7 @@ class Engine:
 
     def last_kernel(self) -> str:
         """The kernel instance the last forward launched, as rocprofv3 names it (include/cet.h
-        cet_last_kernel), e.g. "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, true>" (C2; the fifth
+        cet_last_kernel), e.g. "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false>" (C2; the fifth
         argument is the compile-time row shape: 0 generic, 1 C2, 2 the e_layers [4, 3] stack; the last, the
         decoder on the LDS-DMA weight feed)."""
         n = check(lib.cet_last_kernel(self._h, None, 0), "cet_last_kernel")

@@ -130,7 +130,7 @@ int cet_set_variant(cet_engine* e, int variant);
 enum { CET_PATH_LW = 3, CET_PATH_V4 = 4, CET_PATH_LW_FUSED = 31, CET_PATH_V4_SPLIT = 41 };
 int cet_last_path(cet_engine* e);
 /* The kernel instance the engine's last forward launched, as rocprofv3's kernel trace names it (e.g.
- * "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, true>" for the C2 instance: d_ff, diagnostic
+ * "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false>" for the C2 instance: d_ff, diagnostic
  * outputs, precision, encoder split, the plan's compile-time rows SH (0 generic, 1 C2, 2 the TimingAnalysis
  * e_layers [4, 3] stack), phase stamps, the decoder on the LDS-DMA weight feed), written NUL-terminated into
  * name[buflen]; returns its length (0 before any forward, or after a layer-wise forward of several
