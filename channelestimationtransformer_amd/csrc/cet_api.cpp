@@ -496,9 +496,11 @@ int resolve_precision(cet_engine* e, float qmax, int* out) {
       return fail(CET_E_INVALID, "fp8 activations need an LSQ engine of at most 8 bits (integer grid in e4m3 pairs)");
     if (qmax > 128.f) return fail(CET_E_INVALID, "fp8 weight pairs hold |q| <= 128");
   }
-  if (P == 0 && qmax > 256.f)
+  if ((P == 0 || P == 4) && qmax > 256.f)
     return fail(CET_E_INVALID, "LSQ grid with |q| = " + std::to_string((int)qmax) +
                                    " > 256 is not exact in bf16; use the split-bf16 precision");
+  if (P == 4 && (c.d_ff != 64 || Ld > 48))
+    return fail(CET_E_INVALID, "the mixed precision (bf16 encoder, split-bf16 decoder) needs d_ff 64 and <= 48 decoder rows");
   *out = P;
   return CET_OK;
 }
@@ -527,7 +529,7 @@ int build_informer(cet_engine* e) {
   }
   e->prec = P;
   p.prec = P;
-  if (P == 1) pk.wlo = &e->wblob_lo;
+  if (P == 1 || P == 4) pk.wlo = &e->wblob_lo;   // split bf16 (4: the decoder's layers; the encoder ignores them)
 
   auto lin = [&](const std::string& n) { return e->W(n + ".weight"); };
   // Linear/conv1x1 (possibly several concatenated along the output axis) → GemmDesc
@@ -814,7 +816,8 @@ int build_informer(cet_engine* e) {
   // per CU still fit with it: its HBM latency then overlaps the LDS zeroing; else it is requested
   // before the last encoder norm, into CTX] | [sampler state: in-kernel replay path only]
   {
-    const int RS = v4_rs(P), planes = v4_planes(P);
+    // 4 (mixed): the bf16 layout, the stack output with a lo plane for the split-bf16 decoder
+    const int RS = v4_rs(P), planes = P == 4 ? 2 : v4_planes(P);
     p.lds4_cnt = v4_cnt(P);
     p.lds4_enc = v4_enc(P);
     p.lds4_enc_lo = SP * RS;
@@ -1546,13 +1549,14 @@ static int launch_fused(cet_engine* e, const InformerArgs& a, hipStream_t st) {
   {
     // the instance launch_v4 takes (v4_instance: one decision for both sides)
     const int inst = v4_instance(b, e->prec, e->icfg.d_ff);
+    const int kp = e->prec == 4 ? 0 : e->prec, kd = e->prec == 4 ? 1 : e->prec;   // encoder / decoder precision
     const int sh = inst == V4I_SHAPE || inst == V4I_SHAPE_STAMPS || (inst == V4I_SPLIT && b.shape == V4S_E43) ? b.shape : 0;
     // the decoder weight feed: the bf16 shape instances (and E43's split form) of a plan build_informer accepted
     b.feed = e->feed_ok && e->prec == 0 && sh != 0 ? 1 : 0;
     char nm[160];
-    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %d, %s, %s>", e->icfg.d_ff,
-                  inst == V4I_DIAG ? "true" : "false", e->prec, inst == V4I_SPLIT ? "true" : "false", sh,
-                  inst == V4I_SHAPE_STAMPS ? "true" : "false", b.feed ? "true" : "false");
+    std::snprintf(nm, sizeof nm, "cet::v4::informer_forward_v4<%d, %s, %d, %s, %d, %s, %s, %d>", e->icfg.d_ff,
+                  inst == V4I_DIAG ? "true" : "false", kp, inst == V4I_SPLIT ? "true" : "false", sh,
+                  inst == V4I_SHAPE_STAMPS ? "true" : "false", b.feed ? "true" : "false", kd);
     e->last_kernel = inst == V4I_NONE ? std::string() : std::string(nm);
   }
   return cet_launch_informer_v4(&b, e->prec, e->icfg.d_ff, replay ? p.lds4_bytes_replay : p.lds4_bytes, st);
@@ -1821,7 +1825,9 @@ int cet_set_stamps(cet_engine* e, uint64_t* stamps_dev) {
 int cet_set_precision(cet_engine* e, int prec) {
   if (!e) return fail(CET_E_INVALID, "null engine");
   if (e->kind != 0) return fail(CET_E_INVALID, "precision modes are Informer-engine only");
-  if (prec < -1 || prec > 2) return fail(CET_E_INVALID, "precision must be -1 (auto), 0 (bf16), 1 (split bf16) or 2 (fp8)");
+  if (prec < -1 || prec > 4 || prec == 3)
+    return fail(CET_E_INVALID, "precision must be -1 (auto), 0 (bf16), 1 (split bf16), 2 (fp8) or 4 (bf16 encoder, "
+                               "split-bf16 decoder)");
   if (e->generic && prec != -1 && prec != 0)
     return fail(CET_E_INVALID, "the layer-wise engine (shapes outside the fused kernels) computes in fp32, or in bf16 "
                                "operands in its fused form");

@@ -23,7 +23,12 @@ namespace v4 {
 // -DCET_C2_STAMPS: per-phase cycles of the instance the bench times).
 // FEED: the decoder's weights and bias / LayerNorm vectors arrive by the LDS-DMA weight feed (cet_v4.hpp; the host
 // builds the parameter tiles and checks the plan: cet_api.cpp build_informer).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false, bool FEED = false>
+// PDEC: the decoder's operand precision — P, or split bf16 under a bf16 encoder (P_BF16 / P_X3, the "mixed"
+// policy for genuinely sparse decoders: the encoder at the bf16 rate and two workgroups per CU, the decoder's
+// ProbSparse selection from fp32-level Q·K).  Its images keep the bf16 layout: hi plane in rows 0-47, lo plane in
+// rows 48-95 of XB and CTX; the stack output gets a second plane.
+template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false, bool FEED = false,
+          int PDEC = P>
 __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, const InformerPlan* __restrict__ plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
 #define PL (*fresh(plan))
@@ -54,8 +59,15 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 
   const Img<P> XB{lds + V4L_XB, G::IMG};
   const Img<P> CTXI{lds + v4_ctx(P), G::IMG};                           // attention context / FFN hidden
-  const Img<P> ENC{lds + v4_enc(P), PL.lds4_enc_lo};                    // encoder-stack output
-  const Img<PP> FIN{lds + v4_ctx(P), Geo<PP>::IMG};                      // decoder output (projection input)
+  // the decoder's precision and images (cet_informer4.hpp PDEC)
+  constexpr int PD = PDEC, PPD = plain_of<PD>();
+  constexpr bool MIXD = PD != P;
+  static_assert(!MIXD || (P == P_BF16 && PD == P_X3), "mixed: bf16 encoder, split-bf16 decoder");
+  constexpr int LOD = 48 * G::RS;   // the mixed decoder's lo plane: rows 48-95 of its image
+  const Img<PD> XBd{lds + V4L_XB, MIXD ? LOD : Geo<PD>::IMG};
+  const Img<PD> CTXd{lds + v4_ctx(P), MIXD ? LOD : Geo<PD>::IMG};
+  const Img<PD> ENC{lds + v4_enc(P), PL.lds4_enc_lo};                   // encoder-stack output
+  const Img<PPD> FIN{lds + v4_ctx(P), MIXD ? LOD : Geo<PPD>::IMG};       // decoder output (projection input)
   float* LNP = reinterpret_cast<float*>(lds + v4_scr(P));            // LN partials (alias the scratch)
 #ifdef CET_LN_LAST
   unsigned* LNC = reinterpret_cast<unsigned*>(lds + PL.lds4_lncnt);  // LayerNorm arrival counter
@@ -150,6 +162,12 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
                               : enc0 + pl * PL.lds4_enc_lo + S0 * RS + (j - 2 * n_x) * 16;
       *reinterpret_cast<f32x4*>(q) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if constexpr (MIXD) {
+      // the stack output's lo-plane padded rows (the decoder's lo-plane rows 48-95 of XB / CTX hold the first
+      // encoder layer's finite rows below 90 and the zeroed rows above before the decoder writes them)
+      for (int i = tid_op(); i < n_e; i += NTHREADS)
+        *reinterpret_cast<f32x4*>(enc0 + PL.lds4_enc_lo + S0 * RS + i * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
 #endif
   if (t4 < L0 * C) *reinterpret_cast<f32x4*>(IN + (t4 >> PL.C_shift) * CS + (t4 & (C - 1))) = xe4;
@@ -203,10 +221,14 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 
   constexpr int FRAGS_PER_TILE4 = 4 * WAVE;   // 16-byte lane fragments per n-tile at K = 128
   // the per-head operands of one attention call (AttentionLayer, attn.py:178-209)
-  auto head_io = [&](const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk, uint32_t Wv, GemmDesc dq,
+  // (the images' precision: the encoder's, or the mixed decoder's with its own context image)
+  auto head_io = [&](const auto& Xq, const auto& Xkv, uint32_t Wq, uint32_t Wk, uint32_t Wv, GemmDesc dq,
                      GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal, int mix, float* attn_out) {
-    HeadIO<P> io;
-    io.xq = Xq; io.xkv = Xkv; io.ctx = CTXI; io.wq = Wq; io.wk = Wk; io.wv = Wv;
+    constexpr int PX = std::decay_t<decltype(Xq)>::PREC;
+    HeadIO<PX> io;
+    io.xq = Xq; io.xkv = Xkv; io.wq = Wq; io.wk = Wk; io.wv = Wv;
+    if constexpr (PX == P) io.ctx = CTXI;
+    else io.ctx = CTXd;
     io.dq = dq; io.dk = dk; io.dv = dv;
     io.LQ = LQ; io.LK = LK; io.prob = prob; io.causal = causal; io.mix = mix; io.u = LQ;
     io.cnt = nullptr; io.cnt_stride = 0; io.scr = SCR; io.attn_out = attn_out; io.m_dbg = nullptr;
@@ -214,7 +236,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     return io;
   };
   // the ProbSparse draws of one attention call: u, the multiplicity table (replayed in-kernel or staged)
-  auto call_setup = [&](HeadIO<P>& io, int call, const uint8_t* pre) __attribute__((always_inline)) {
+  auto call_setup = [&](auto& io, int call, const uint8_t* pre) __attribute__((always_inline)) {
 #ifndef CET_STAMP_DEC_CALL
     io.st = (stamps && call >= 0 && call < 2) ? stamps + 100 + 8 * call : nullptr;
 #else   // diagnostic: sub-phases of the first encoder call and the first decoder self-attention call
@@ -253,21 +275,22 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
   // one head per wave; MQc / MKc: compile-time bounds on the query / key tiles; NKXc: whether MKc is
   // exactly ceil(LK / 16) (true for the encoder, which has a case for every nmt, and for the decoder
   // self-attention, whose bound is its own length; the un-hoisted cross-attention passes it per bound)
-  auto attend = [&](auto MQc, auto MKc, auto NKXc, const Img<P>& Xq, const Img<P>& Xkv, uint32_t Wq, uint32_t Wk,
+  auto attend = [&](auto MQc, auto MKc, auto NKXc, const auto& Xq, const auto& Xkv, uint32_t Wq, uint32_t Wk,
                     uint32_t Wv, GemmDesc dq, GemmDesc dk, GemmDesc dv, int LQ, int LK, int prob, int causal,
                     int mix, int call, float* attn_out, const uint8_t* pre = nullptr) {
     constexpr int MQ_ = decltype(MQc)::value, MK_ = decltype(MKc)::value;
     constexpr bool NKX_ = decltype(NKXc)::value;
-    HeadIO<P> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
+    constexpr int PX = std::decay_t<decltype(Xq)>::PREC;
+    HeadIO<PX> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
 #ifdef CET_AB8
     // reproduction of round 4's ab8 candidate: the head's K/V weights requested before
     // the call's table setup; it made the split-bf16 production instance disagree with its diagnostic one
-    const KVPre<P> kvp = prefetch_kv<P>(io, M, w);
+    const KVPre<PX> kvp = prefetch_kv<PX>(io, M, w);
     call_setup(io, call, pre);
-    attention_head<P, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
+    attention_head<PX, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
 #else
     call_setup(io, call, pre);
-    attention_head<P, MQ_, MK_, false, NKX_>(io, M, w);
+    attention_head<PX, MQ_, MK_, false, NKX_>(io, M, w);
 #endif
   };
 
@@ -522,7 +545,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     if constexpr (FEED && !SPLIT) {
       if (e == PL.n_enc - 1) fd_prefill();
     }
-    const ImgRows<P> encw{ENC, PL.enc_row_off[e]};
+    const ImgRows<PD> encw{ENC, PL.enc_row_off[e]};
     ln_res(X, nmt, rows, M, PL.enc_norm[e], 1e-5f, false, LNP, XB, &encw, nullptr, LNC);
     __syncthreads();
     if (dbg && PL.enc_dbg[e] >= 0) dump_res(X, nmt, rows, dbg + PL.enc_dbg[e]);
@@ -752,14 +775,14 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     Res<NMD> XD;
     {
       const GemmDesc d = PL.emb_dec;
-      gemm_res_n<PP, 2, NMD>(M, d, LoadEmbed<PP>{XDEC, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
+      gemm_res_n<PPD, 2, NMD>(M, d, LoadEmbed<PPD>{XDEC, Ld, PL.C_shift, CS, 0}, [&](int mt, int n0, f32x4 y) {
         const int m = mt * 16 + (lane_op() & 15);
         const int prow = m < LMAX ? m : LMAX - 1;
         XD.v[mt] = y + pload4(M, PL.pe_dec, prow * DMODEL + n0);
       });
     }
     __syncthreads();
-    store_res(XD, nmd, Ld, XB);
+    store_res(XD, nmd, Ld, XBd);
     __syncthreads();
     if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_emb);
     STAMP();  // decoder embedding
@@ -774,67 +797,67 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
       // self-attention, so their weight fetch overlaps it instead of following it (123.4 vs 124.3 us,
       // profiles/r02/ab_cross_hoist.log)
       const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
-      const HeadIO<P> cio = head_io(XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0), part_of(ckv, 0),
+      const HeadIO<PD> cio = head_io(XBd, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0), part_of(ckv, 0),
                                     part_of(ckv, 128), Ld, S, 0, 0, 0, nullptr);
-      AF<PP> CK[NMS], CV[NMS];
-      project_kv<P, NMS>(cio, M, w, CK, CV);
+      AF<PPD> CK[NMS], CV[NMS];
+      project_kv<PD, NMS>(cio, M, w, CK, CV);
 #endif
       {
         // masked self-attention with the mix scramble (model.py:211-222)
         const GemmDesc q = DLD.qkv;
-        attend(IC<NMD>{}, IC<NMD>{}, std::true_type{}, XB, XB, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
+        attend(IC<NMD>{}, IC<NMD>{}, std::true_type{}, XBd, XBd, q.w, q.w + 8 * FRAGS_PER_TILE4, q.w + 16 * FRAGS_PER_TILE4,
                part_of(q, 0), part_of(q, 128), part_of(q, 256), Ld, Ld, PL.prob, 1, PL.mix, DLD.call, nullptr);
       }
-      const WPre<P, 4> po = prefetch_res<P, 4>(M, DLD.o);
+      const WPre<PD, 4> po = prefetch_res<PD, 4>(M, DLD.o);
       __syncthreads();
       STAMP();  // decoder self-attention
-      gemm_res_n<P, 4, NMD>(po, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      gemm_res_n<PD, 4, NMD>(po, LoadImg<PD>{CTXd}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
 #ifndef CET_NO_CROSSQ_PRE
       // the cross-attention's Q weights of head w, requested before LN1's barrier (the decoder's residual
       // is one tile: the registers are free here)
-      const WPre<P, 4> pcq = prefetch_res<P, 4>(M, cq);
-      const WPre<P, 4>* cqp = &pcq;
+      const WPre<PD, 4> pcq = prefetch_res<PD, 4>(M, cq);
+      const WPre<PD, 4>* cqp = &pcq;
 #else
-      const WPre<P, 4>* cqp = nullptr;
+      const WPre<PD, 4>* cqp = nullptr;
 #endif
-      ln_res(XD, nmd, Ld, M, DLD.ln1, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      ln_res(XD, nmd, Ld, M, DLD.ln1, 1e-5f, false, LNP, XBd, (const Img<PD>*)nullptr);
       __syncthreads();
       {
         // cross-attention: FullAttention over the encoder-stack output, mix=False
 #ifndef CET_NO_CROSS_HOIST
-        attention_head<P, NMD, NMS, true, CROSS_EXACT>(cio, M, w, CK, CV, cqp);
+        attention_head<PD, NMD, NMS, true, CROSS_EXACT>(cio, M, w, CK, CV, cqp);
 #else
         const GemmDesc cq = DLD.cq, ckv = DLD.ckv;
         // the key-tile bound MT is exact only for S in 81-96; NMS == 1 is exact (S ≤ 16)
-        attend(IC<NMD>{}, IC<NMS>{}, std::bool_constant<NMS == 1>{}, XB, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
+        attend(IC<NMD>{}, IC<NMS>{}, std::bool_constant<NMS == 1>{}, XBd, ENC, cq.w, ckv.w, ckv.w + 8 * FRAGS_PER_TILE4, part_of(cq, 0),
                part_of(ckv, 0), part_of(ckv, 128), Ld, S, 0, 0, 0, -1, nullptr);
 #endif
       }
-      const WPre<P, 4> pco = prefetch_res<P, 4>(M, DLD.co);
+      const WPre<PD, 4> pco = prefetch_res<PD, 4>(M, DLD.co);
       __syncthreads();
       STAMP();  // cross-attention
-      gemm_res_n<P, 4, NMD>(pco, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
-      const WPre<P, 4> pf1 = prefetch_tiles<P, 4>(M, DLD.f1, DFF / 16);
-      ln_res(XD, nmd, Ld, M, DLD.ln2, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      gemm_res_n<PD, 4, NMD>(pco, LoadImg<PD>{CTXd}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      const WPre<PD, 4> pf1 = prefetch_tiles<PD, 4>(M, DLD.f1, DFF / 16);
+      ln_res(XD, nmd, Ld, M, DLD.ln2, 1e-5f, false, LNP, XBd, (const Img<PD>*)nullptr);
       __syncthreads();
       {
         const int relu = PL.act_relu;
-        gemm_tiles1<P, 4>(pf1, DFF / 16, nmd, LoadImg<P>{XB}, [&](int mt, int n0, f32x4 v) {
+        gemm_tiles1<PD, 4>(pf1, DFF / 16, nmd, LoadImg<PD>{XBd}, [&](int mt, int n0, f32x4 v) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = relu ? fmaxf(v[r], 0.f) : gelu_erf(v[r]);
-          CTXI.st4(mt * 16 + (lane_op() & 15), n0, v);
+          CTXd.st4(mt * 16 + (lane_op() & 15), n0, v);
         });
       }
-      const WPre<P, DFF / 32> pf2 = prefetch_res<P, DFF / 32>(M, DLD.f2);
+      const WPre<PD, DFF / 32> pf2 = prefetch_res<PD, DFF / 32>(M, DLD.f2);
       __syncthreads();
-      gemm_res_n<P, DFF / 32, NMD>(pf2, LoadImg<P>{CTXI}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
-      ln_res(XD, nmd, Ld, M, DLD.ln3, 1e-5f, false, LNP, XB, (const Img<P>*)nullptr);
+      gemm_res_n<PD, DFF / 32, NMD>(pf2, LoadImg<PD>{CTXd}, [&](int mt, int n0, f32x4 y) { XD.v[mt] += y; });
+      ln_res(XD, nmd, Ld, M, DLD.ln3, 1e-5f, false, LNP, XBd, (const Img<PD>*)nullptr);
       __syncthreads();
       STAMP();  // decoder O/LN1 + cross O/LN2 + FFN/LN3
       if (dbg && DLD.dbg >= 0) dump_res(XD, nmd, Ld, dbg + DLD.dbg);
     }
     // final norm → the projection's input image (plain precision; CTX is free: FFN2 is done)
-    ln_res(XD, nmd, Ld, M, PL.dec_norm, 1e-5f, false, LNP, FIN, (const Img<PP>*)nullptr);
+    ln_res(XD, nmd, Ld, M, PL.dec_norm, 1e-5f, false, LNP, FIN, (const Img<PPD>*)nullptr);
     __syncthreads();
     if (dbg) dump_res(XD, nmd, Ld, dbg + PL.dbg_dec_out);
     {
@@ -847,7 +870,7 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 #else
       const bool fuse = a.label != nullptr;   // the launcher guarantees c_out ≤ 16 (one n-tile)
 #endif
-      gemm_tiles<PP, 4>(M, d, d.n / 16, nmd, LoadImg<PP>{FIN}, [&](int mt, int n0, f32x4 v) {
+      gemm_tiles<PPD, 4>(M, d, d.n / 16, nmd, LoadImg<PPD>{FIN}, [&](int mt, int n0, f32x4 v) {
         const int lane = lane_op();
         const int m = mt * 16 + (lane & 15);
         const bool valid = m >= first_row && m < Ld;
@@ -978,10 +1001,11 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
 }
 
 // X3 carries hi/lo operand pairs: 256 VGPRs, one workgroup per CU; the others fit 128 (two per CU).
-template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false, bool FEED = false>
+template <int DFF, bool DIAG, int P, bool SPLIT = false, int SH = 0, bool ST = false, bool FEED = false,
+          int PDEC = P>
 __global__ void __launch_bounds__(NTHREADS, P == P_X3 ? 2 : 4)
     informer_forward_v4(InformerArgs a, const InformerPlan* __restrict__ plan) {
-  informer_forward_v4_body<DFF, DIAG, P, SPLIT, SH, ST, FEED>(a, plan);
+  informer_forward_v4_body<DFF, DIAG, P, SPLIT, SH, ST, FEED, PDEC>(a, plan);
 }
 
 template <int P>
@@ -1033,6 +1057,25 @@ int launch_v4(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream)
   args.lds_bytes = lds_bytes;
   const unsigned grid = (unsigned)a->B * (split ? (unsigned)a->enc_split : 1u);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHREADS), lds_bytes, stream, args, a->plan);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The mixed policy (host precision 4): the bf16 encoder with a split-bf16 decoder (PDEC = P_X3).
+inline int launch_v4_mix(const InformerArgs* a, int dff, int lds_bytes, hipStream_t stream) {
+  if (a->B <= 0) return 0;
+  using K = void (*)(InformerArgs, const InformerPlan*);
+  K kern = nullptr;
+  switch (v4_instance(*a, 4, dff)) {
+    case V4I_SHAPE: kern = informer_forward_v4<64, false, P_BF16, false, V4S_C2, false, false, P_X3>; break;
+    case V4I_DIAG: kern = informer_forward_v4<64, true, P_BF16, false, V4S_GENERIC, false, false, P_X3>; break;
+    case V4I_GENERIC: kern = informer_forward_v4<64, false, P_BF16, false, V4S_GENERIC, false, false, P_X3>; break;
+    default: break;
+  }
+  if (!kern) return -3;
+  if (!ensure_lds_attr(reinterpret_cast<const void*>(kern))) return -1;
+  InformerArgs args = *a;
+  args.lds_bytes = lds_bytes;
+  hipLaunchKernelGGL(kern, dim3((unsigned)a->B), dim3(NTHREADS), lds_bytes, stream, args, a->plan);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

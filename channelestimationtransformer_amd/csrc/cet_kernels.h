@@ -63,6 +63,7 @@ __host__ __device__ inline int v4_instance(const InformerArgs& a, int prec, int 
 #endif
   // compile-time rows: C2 for bf16 and fp8, E43 for bf16
   if (dff == 64 && !diag && ((a.shape == V4S_C2 && prec != 1) || (a.shape == V4S_E43 && prec == 0))) return V4I_SHAPE;
+  if (prec == 4 && dff != 64) return V4I_NONE;   // the mixed instances exist for d_ff 64
   return diag ? V4I_DIAG : V4I_GENERIC;
 }
 

@@ -182,6 +182,7 @@ struct ImgBase<P_FP8> {
 };
 template <int P>
 struct Img : ImgBase<P> {
+  static constexpr int PREC = P;
   using ImgBase<P>::base;
   using ImgBase<P>::lo;
   __device__ __forceinline__ Img(char* b, int l) {

@@ -206,7 +206,7 @@ class Engine:
 
     def last_kernel(self) -> str:
         """The kernel instance the last forward launched, as rocprofv3 names it (include/cet.h
-        cet_last_kernel), e.g. "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false>" (C2; the fifth
+        cet_last_kernel), e.g. "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false, 0>" (C2; the fifth
         argument is the compile-time row shape: 0 generic, 1 C2, 2 the e_layers [4, 3] stack; the last, the
         decoder on the LDS-DMA weight feed)."""
         n = check(lib.cet_last_kernel(self._h, None, 0), "cet_last_kernel")
@@ -214,10 +214,11 @@ class Engine:
         check(lib.cet_last_kernel(self._h, buf, n + 1), "cet_last_kernel")
         return buf.value.decode()
 
-    PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3}
+    PRECISIONS = {"auto": -1, "bf16": 0, "split-bf16": 1, "fp8": 2, "fp32-layerwise": 3, "mixed": 4}
 
     def set_precision(self, prec) -> None:
-        """Dense-layer operand precision of the v4 kernel: "auto", "bf16", "split-bf16" or "fp8" (include/cet.h).
+        """Dense-layer operand precision of the v4 kernel: "auto", "bf16", "split-bf16", "fp8" or "mixed" (a bf16
+        encoder with a split-bf16 decoder; include/cet.h).
         Engines on the layer-wise path (shapes outside the fused kernels) report "fp32-layerwise"."""
         code = self.PRECISIONS[prec] if isinstance(prec, str) else int(prec)
         check(lib.cet_set_precision(self._h, code), "cet_set_precision")

@@ -130,9 +130,10 @@ int cet_set_variant(cet_engine* e, int variant);
 enum { CET_PATH_LW = 3, CET_PATH_V4 = 4, CET_PATH_LW_FUSED = 31, CET_PATH_V4_SPLIT = 41 };
 int cet_last_path(cet_engine* e);
 /* The kernel instance the engine's last forward launched, as rocprofv3's kernel trace names it (e.g.
- * "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false>" for the C2 instance: d_ff, diagnostic
+ * "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false, 0>" for the C2 instance: d_ff, diagnostic
  * outputs, precision, encoder split, the plan's compile-time rows SH (0 generic, 1 C2, 2 the TimingAnalysis
- * e_layers [4, 3] stack), phase stamps, the decoder on the LDS-DMA weight feed), written NUL-terminated into
+ * e_layers [4, 3] stack), phase stamps, the decoder on the LDS-DMA weight feed, the decoder's precision),
+ * written NUL-terminated into
  * name[buflen]; returns its length (0 before any forward, or after a layer-wise forward of several
  * operator launches).  No reference counterpart: measurement plumbing (bench.py's roofline.kernel). */
 int cet_last_kernel(cet_engine* e, char* name, int buflen);
@@ -152,6 +153,8 @@ int cet_last_kernel(cet_engine* e, char* name, int buflen);
  *      engine "auto" keeps fp32 and 0 selects bf16 GEMM operands (fp32 accumulation, LayerNorm and
  *      attention) in its fused one-launch form (cet_lwf.hip; feature counts multiples of 8): a forward
  *      outside that form then fails with CET_E_INVALID; 1 and 2 are refused.
+ *    4 mixed: the encoder in bf16 (two workgroups per CU) and the decoder in split bf16 — for genuinely
+ *      sparse masked decoders, whose top-u selection needs fp32-level Q·K (d_ff 64, <= 48 decoder rows).
  * cet_get_precision() returns the precision the packed plan uses (packs the weights if needed).
  * Replaces nothing in the reference, which computes in fp32 (FullPrecision/InformerModel) or with
  * fp32 fake-quantised weights (models/InformerLSQ/LSQ.py:65-74). */

@@ -132,7 +132,7 @@ def test_c2_instance_b512_under_lds_poison(attn):
         return out.cpu().numpy(), sums.cpu().numpy()
 
     (p_out, p_sums), (q_out, q_sums) = _twice(run)
-    assert eng.last_kernel() == "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false>"
+    assert eng.last_kernel() == "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false, 0>"
     assert np.isfinite(q_out).all()
     np.testing.assert_array_equal(q_out, p_out)
     np.testing.assert_array_equal(q_sums, p_sums)

@@ -161,6 +161,9 @@ def main():
          informer_flops(seq_len=25, d_model=64, e_layers=(4, 3), attn="full"), dict(precision="bf16"), "bf16"),
         ("lab20 FullPrecision InformerStack label_len=20 (sparse 25-row decoder; auto precision: split bf16)",
          lambda: informer(dev, [4], "prob", label_len=20), 512, informer_flops(label_len=20), {}, "bf16"),
+        ("lab20 FullPrecision InformerStack label_len=20 (sparse 25-row decoder), mixed: bf16 encoder, split-bf16 "
+         "decoder", lambda: informer(dev, [4], "prob", label_len=20), 512, informer_flops(label_len=20),
+         dict(precision="mixed"), "bf16"),
     ]
     tol = {"fp8": 2e-3}   # rel-NMSE bar: north_star's 1e-4, the self-set fp8 bar for C5 fp8
     for name, mk, B, flops, kw, peak in runs:

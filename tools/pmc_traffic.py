@@ -30,7 +30,7 @@ def per_dispatch(path, counter, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="informer_forward_v4<64, false, 0, false, 1, false, false>")
+    ap.add_argument("--kernel", default="informer_forward_v4<64, false, 0, false, 1, false, false, 0>")
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--io-bytes-per-seq", type=int, default=7040)
     ap.add_argument("-o", "--out", required=True)

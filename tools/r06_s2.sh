@@ -1,10 +1,12 @@
-# round-6 session 2: the default library's GPU suite (poison tests included), the ab8 candidate plain and under
-# the LDS poison, and the LN_LAST A/B (C2 bench, E43 config, C2 stamps)
+# round-6 session 2: the default library's GPU suite (poison, lab20 mixed and feed tests included), the ab8
+# candidate plain and under the LDS poison, the lab20 mixed measurement, and the LN_LAST A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r06s2; mkdir -p $O
 L=channelestimationtransformer_amd
-timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1; echo "default suite rc $?"; tail -3 $O/gpu_tests.log
+timeout -k 10 800 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1; echo "default suite rc $?"; tail -3 $O/gpu_tests.log; grep FAILED $O/gpu_tests.log | head
+timeout -k 10 300 python tools/lab20_mixed.py 512 > $O/lab20_mixed.json 2> $O/lab20_mixed.err; echo "lab20 mixed rc $?"; cat $O/lab20_mixed.json
+timeout -k 10 400 python tools/bench_configs.py --only lab20 > $O/configs_lab20.jsonl 2> $O/configs_lab20.err; echo "configs rc $?"; cut -c1-400 $O/configs_lab20.jsonl
 K="split_bf16_is_fp32_parity or reference_fixture"
 CET_LIB=$(pwd)/$L/libcet_ab8.so timeout -k 10 300 python -u -m pytest tests/test_gpu_informer.py -k "$K" -v --timeout 120 --timeout-method thread > $O/ab8_plain.log 2>&1; echo "ab8 plain rc $?"; grep -E "passed|failed" $O/ab8_plain.log | tail -2
 CET_LDS_POISON=1 CET_LIB=$(pwd)/$L/libcet_ab8.so timeout -k 10 300 python -u -m pytest tests/test_gpu_informer.py -k "$K" -v --timeout 120 --timeout-method thread > $O/ab8_poison.log 2>&1; echo "ab8 poison rc $?"; grep -E "passed|failed" $O/ab8_poison.log | tail -2
