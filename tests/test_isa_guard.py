@@ -70,7 +70,13 @@ def test_scan_flags_swaps_in_divergent_regions(lines, flag):
 # loops stopped hoisting their per-lane addresses (136 B before, which wrote 26 MiB of spill
 # scratch per launch).  A regression past this budget brings the spill traffic back.
 SCRATCH_BUDGET = {
-    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0E": 64,    # C2 production (bf16)
+    # the bf16 production instances (generic, C2, E43, encoder split; register-path decoder, bf16 decoder)
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi0ELb0ELb0ELi0E": 64,
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi1ELb0ELb0ELi0E": 64,    # C2 production (bf16)
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi2ELb0ELb0ELi0E": 64,
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb1E": 64,
+    # the mixed policy (bf16 encoder, split-bf16 decoder at the 128-VGPR cap: the decoder's hi/lo operands spill)
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi1ELb0ELb0ELi1E": 400,
     "_ZN3cet2v422transformer_forward_v4ILi64ELb0E": 16,         # C3 production
     # fused layer-wise form, d_model <= 64: 16-24 B until round 5; 52 B (≤ 17 VGPRs) with the register attention
     # inlined at its three call sites, which runs a d_model-64, 4-head plan 17 % (fp32) / 25 % (bf16) faster
