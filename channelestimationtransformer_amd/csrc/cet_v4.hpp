@@ -1052,6 +1052,11 @@ __device__ __forceinline__ void project_kv(const HeadIO<PD>& io, const KVPre<PD>
         k = mma<PD>(&w.k[ks], bx, k);
         v = mma_xw<PD>(bx, &w.v[ks], v);
       }
+#ifdef CET_MFMA_NOP
+      // diagnostic (the ab8 investigation): 32 extra wait states between the K / V MFMA chains and
+      // the VALU epilogue that reads their results
+      asm volatile("s_nop 15\n\ts_nop 15" : "+v"(k), "+v"(v));
+#endif
       Kf[mt] = split4<PA>(k * w.sk + w.bk);
       Vf[mt] = split4<PA>(v * w.sv + w.bv);
     }
