@@ -287,7 +287,15 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     // the call's table setup; it made the split-bf16 production instance disagree with its diagnostic one
     const KVPre<PX> kvp = prefetch_kv<PX>(io, M, w);
     call_setup(io, call, pre);
+#ifndef CET_AB8_EXTKV
     attention_head<PX, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
+#else
+    // the same request order with the K / V tiles projected here and handed over in registers (the build above
+    // keeps the address-taken weight struct in private memory)
+    AF<plain_of<PX>()> Kf[MK_], Vf[MK_];
+    project_kv<PX, MK_>(io, kvp, Kf, Vf);
+    attention_head<PX, MQ_, MK_, true, NKX_>(io, M, w, Kf, Vf);
+#endif
 #else
     call_setup(io, call, pre);
     attention_head<PX, MQ_, MK_, false, NKX_>(io, M, w);

@@ -75,6 +75,12 @@ SCRATCH_BUDGET = {
     "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi1ELb0ELb0ELi0E": 64,    # C2 production (bf16)
     "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi2ELb0ELb0ELi0E": 64,
     "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb1E": 64,
+    # the split-bf16 production instances: no private memory at all.  The round-4 ab8 reordering's wrong element
+    # travelled with its address-taken K/V weight struct kept in private memory (320 B per lane here, 60 scratch
+    # stores and 228 scratch loads), so a split-bf16 instance that grows a private segment is the
+    # first thing to look at
+    "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi1ELb0E": 0,
+    "_ZN3cet2v419informer_forward_v4ILi128ELb0ELi1ELb0E": 0,
     # the mixed policy (bf16 encoder, split-bf16 decoder at the 128-VGPR cap: the decoder's hi/lo operands spill)
     "_ZN3cet2v419informer_forward_v4ILi64ELb0ELi0ELb0ELi1ELb0ELb0ELi1E": 400,
     "_ZN3cet2v422transformer_forward_v4ILi64ELb0E": 16,         # C3 production
