@@ -1114,6 +1114,11 @@ __device__ __forceinline__ void attention_head(const HeadIO<PD>& io, const Mem& 
       Vf[mt] = vin[mt];
     }
   } else if (kvpre) {
+#ifdef CET_AB8_INV
+    // diagnostic: invalidate the vector L1 before the caller's struct is read back from private
+    // memory — does the ab8 build's wrong element come from a stale L1 line?
+    asm volatile("buffer_inv sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+#endif
     project_kv<PD, MK>(io, *kvpre, Kf, Vf);   // weights requested by the caller (the CET_AB8 reproduction)
   } else {
     project_kv<PD, MK>(io, m, h, Kf, Vf);
