@@ -1,5 +1,5 @@
-# round-6 session 11: schedule-driven priority for the two workgroups of a CU (a throw-away build, -DCET_SCHED_PRIO=T:
-# ticks of the 100 MHz clock per workgroup) against the default build, alternated on one box
+# round-6 session 11: schedule-driven priority for the two workgroups of a CU (a throw-away build of
+# -DCET_SCHED_PRIO=T, T = target ticks of the 100 MHz clock per workgroup) against the default build
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r06s11; mkdir -p $O
