@@ -315,6 +315,39 @@ def test_prepared_tables_continue_the_stream():
         np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{i + 1} (B={B})")
 
 
+def test_device_sampler_prepared_tables_with_batches_past_one_wave():
+    """Batches larger than the 512 workgroup slots (a second wave of workgroups starts while the first is still
+    running) on the device-resident sampler with prepared tables: the first workgroup to finish prepares the next
+    forward's tables while later workgroups of the current forward still read this one's.  Every forward must
+    consume exactly torch.randint's draws — bitwise against explicit-index runs of the same batches."""
+    _gpu()
+    from engine_util import model_for, run_engine
+
+    case = load_case("informer_prob_b4")
+    m = model_for(case)
+    dev = torch.device("cuda:0")
+    eng = m.engine(dev)
+    xe_np = np.ascontiguousarray(np.tile(case.z["x_enc"], (258, 1, 1)))   # 1,032 sequences
+    xd_np = np.ascontiguousarray(np.tile(case.z["x_dec"], (258, 1, 1)))
+    xe, xd = torch.from_numpy(xe_np).to(dev), torch.from_numpy(xd_np).to(dev)
+    seed = 4099
+    shapes = eng.prob_calls()
+    torch.manual_seed(seed)
+    plan = [1031, 1031, 600, 513, 1031]
+    draws = [[torch.randint(lk, shp).numpy() for lk, shp in shapes] for _ in plan]
+    eng.seed(seed)
+    outs = []
+    for B in plan:
+        o = torch.empty(B, 5, 16, device=dev)
+        eng.forward(xe[:B].contiguous(), xd[:B].contiguous(), o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        B = o.shape[0]
+        ref, _, _ = run_engine(m, xe_np[:B], xd_np[:B], draws[i])
+        np.testing.assert_array_equal(o.cpu().numpy(), ref, err_msg=f"forward #{i + 1} (B={B})")
+
+
 def test_host_and_device_samplers_share_the_stream():
     """cet_set_sampler switches the native draws between the device-resident mt19937 and the host
     mirror mid-stream (with prepared tables pending); every forward still consumes exactly the
