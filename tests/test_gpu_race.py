@@ -34,7 +34,8 @@ def _gpu():
     # its spilled hi / lo decoder operands): bitwise stability only — its distance from the reference on random
     # batches is a precision property (near-tie selections), not what this test is about
     ("informer_prob_lab20", "mixed", "cet::v4::informer_forward_v4<64, false, 0, false, 1, false, false, 1>", None),
-], ids=["c2-bf16", "c2-split-bf16", "e43-bf16", "e43-split-bf16", "lab20-mixed"])
+    ("transformer_c3", None, "cet::v4::transformer_forward_v4<64, false, true>", TOL),   # C3 (no precision modes)
+], ids=["c2-bf16", "c2-split-bf16", "e43-bf16", "e43-split-bf16", "lab20-mixed", "c3"])
 def test_output_independent_of_timing_and_placement(name, precision, kernel, tol):
     _gpu()
     from engine_util import model_for
@@ -53,7 +54,8 @@ def test_output_independent_of_timing_and_placement(name, precision, kernel, tol
     for _ in range(2):
         m = model_for(case)
         e = m.engine(dev)
-        e.set_precision(precision)
+        if precision is not None:
+            e.set_precision(precision)
         engs.append(e)
 
     def fwd(i, x, y, out, stream=None):
@@ -72,7 +74,11 @@ def test_output_independent_of_timing_and_placement(name, precision, kernel, tol
     assert np.isfinite(ref_np).all()
     if tol is not None:
         rows = np.r_[0:8, B - 8:B]
-        oref, _ = oracle_for(case).forward(xe_np[rows], xd_np[rows], case.idx)
+        orc = oracle_for(case)
+        if case.meta["model"] == "transformer":
+            oref = orc.forward(xe_np[rows], xd_np[rows])
+        else:
+            oref, _ = orc.forward(xe_np[rows], xd_np[rows], case.idx)
         assert rel_nmse(ref_np[rows], oref) < tol
 
     # every buffer the side streams touch is made (on the default stream) and kept alive before they start
