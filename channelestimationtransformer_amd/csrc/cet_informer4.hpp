@@ -282,20 +282,22 @@ __device__ __forceinline__ void informer_forward_v4_body(const InformerArgs& a, 
     constexpr bool NKX_ = decltype(NKXc)::value;
     constexpr int PX = std::decay_t<decltype(Xq)>::PREC;
     HeadIO<PX> io = head_io(Xq, Xkv, Wq, Wk, Wv, dq, dk, dv, LQ, LK, prob, causal, mix, attn_out);
-#ifdef CET_AB8
-    // reproduction of round 4's ab8 candidate: the head's K/V weights requested before
-    // the call's table setup; it made the split-bf16 production instance disagree with its diagnostic one
+#if defined(CET_AB8)
+    // reproduction of round 4's ab8 candidate: the early request below with the weight struct handed
+    // to attention_head by address — the split-bf16 production instance then keeps it in private memory and
+    // disagrees with its diagnostic instance
     const KVPre<PX> kvp = prefetch_kv<PX>(io, M, w);
     call_setup(io, call, pre);
-#ifndef CET_AB8_EXTKV
     attention_head<PX, MQ_, MK_, false, NKX_>(io, M, w, nullptr, nullptr, nullptr, &kvp);
-#else
-    // the same request order with the K / V tiles projected here and handed over in registers (the build above
-    // keeps the address-taken weight struct in private memory)
+#elif !defined(CET_LATE_KV)
+    // the head's K/V weights are requested before the call's table setup (its copy loop and barrier hide their L2
+    // round trip), and the K/V tiles are projected here and handed to attention_head in registers: +1.4 % seq/s
+    // at the driver's bench command, +1.6 % at 300 steps, kernel alone +0.8 µs (profiles/r06/early_kv/)
+    const KVPre<PX> kvp = prefetch_kv<PX>(io, M, w);
+    call_setup(io, call, pre);
     AF<plain_of<PX>()> Kf[MK_], Vf[MK_];
     project_kv<PX, MK_>(io, kvp, Kf, Vf);
     attention_head<PX, MQ_, MK_, true, NKX_>(io, M, w, Kf, Vf);
-#endif
 #else
     call_setup(io, call, pre);
     attention_head<PX, MQ_, MK_, false, NKX_>(io, M, w);
